@@ -1,0 +1,130 @@
+"""ctypes binding of libergm_hip.so (the C-ABI declared in include/ergm_hip.h).
+
+The library is loaded from the package directory (built in-tree by ``ergm_amd/build.py``).  There
+is no fallback: if the library is missing or fails to load, every op raises — the product path never
+silently runs on CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
+
+ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
+F32, BF16 = 0, 1
+MK, KM = 0, 1
+NK, KN = 0, 1
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GELU_BWD, EPI_ACCUM = range(6)
+LAYER_TENSORS = ["ln_1.weight", "ln_1.bias", "attn.c_attn.weight", "attn.c_attn.bias", "attn.c_proj.weight",
+                 "attn.c_proj.bias", "ln_cross_attn.weight", "ln_cross_attn.bias",
+                 "crossattention.q_attn.weight", "crossattention.q_attn.bias", "crossattention.c_proj.weight",
+                 "crossattention.c_proj.bias", "ln_2.weight", "ln_2.bias", "mlp.c_fc.weight", "mlp.c_fc.bias",
+                 "mlp.c_proj.weight", "mlp.c_proj.bias"]  # order of ergm_layer_tensor
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
+                ("ldc", C.c_int), ("a_layout", C.c_int), ("b_layout", C.c_int), ("c_dtype", C.c_int),
+                ("epilogue", C.c_int), ("alpha", C.c_float), ("bias", C.c_void_p), ("aux", C.c_void_p),
+                ("ld_aux", C.c_int), ("aux_out", C.c_void_p), ("ld_aux_out", C.c_int), ("split_k", C.c_int),
+                ("alpha_dev", C.c_void_p)]
+
+
+class ModelDims(C.Structure):
+    _fields_ = [("vocab", C.c_int), ("vocab_pad", C.c_int), ("n_embd", C.c_int), ("n_layer", C.c_int),
+                ("n_head", C.c_int), ("n_inner", C.c_int), ("n_positions", C.c_int), ("batch", C.c_int),
+                ("seq", C.c_int), ("eps", C.c_float), ("has_features", C.c_int), ("ld_vis", C.c_int)]
+
+
+class ModelParams(C.Structure):
+    _fields_ = [("wte", C.c_void_p), ("wte_b", C.c_void_p), ("wpe", C.c_void_p), ("ln_f_w", C.c_void_p),
+                ("ln_f_b", C.c_void_p), ("emo_w", C.c_void_p), ("capkv_w_b", C.c_void_p), ("capkv_b", C.c_void_p),
+                ("layer_f32", C.c_void_p), ("layer_b16", C.c_void_p), ("layer_stride", C.c_int64),
+                ("layer_off", C.c_int64 * 18),
+                ("g_wte", C.c_void_p), ("g_wpe", C.c_void_p), ("g_ln_f_w", C.c_void_p), ("g_ln_f_b", C.c_void_p),
+                ("g_emo_w", C.c_void_p), ("g_capkv_w", C.c_void_p), ("g_capkv_b", C.c_void_p),
+                ("g_layer", C.c_void_p)]
+
+
+vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
+_SIGS = {
+    "ergm_version": (i32, []),
+    "ergm_last_error": (i32, [C.c_char_p, sz]),
+    "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
+    "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
+    "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),
+    "ergm_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, f32, vp]),
+    "ergm_layernorm_bwd_workspace_size": (sz, [i32, i32]),
+    "ergm_layernorm_bwd": (i32, [vp] * 11 + [sz, i32, i32, vp]),
+    "ergm_colsum_workspace_size": (sz, [i32, i32]),
+    "ergm_colsum": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
+    "ergm_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "ergm_embed_bwd_workspace_size": (sz, [i32]),
+    "ergm_embed_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, vp]),
+    "ergm_count_valid": (i32, [vp, i32, i32, vp, vp]),
+    "ergm_xent_fwd_bwd": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
+    "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
+    "ergm_loss_finalize": (i32, [vp, i32, vp, vp, i32, vp, vp]),
+    "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, vp]),
+    "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
+    "ergm_axpy": (i32, [vp, vp, sz, f32, vp]),
+    "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
+    "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
+    "ergm_model_destroy": (i32, [vp]),
+    "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
+    "ergm_model_forward": (i32, [vp, vp, vp, vp, i32, vp]),
+    "ergm_model_backward_head": (i32, [vp, vp, vp]),
+    "ergm_model_backward_layer": (i32, [vp, i32, vp]),
+    "ergm_model_backward_embed": (i32, [vp, vp]),
+}
+EXPORTED = sorted(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class ErgmError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the library; raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise ErgmError(f"libergm_hip.so not found at {path}: run `python -m ergm_amd.build` "
+                                "(the HIP path has no CPU fallback)")
+            lib = C.CDLL(path)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(512)
+    load().ergm_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    """Map a C status to the reference's exception types (ValueError for bad arguments)."""
+    if rc == ERGM_OK:
+        return
+    msg = f"{what}: {last_error()}"
+    if rc == ERGM_EINVAL:
+        raise ValueError(msg)
+    if rc == ERGM_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise ErgmError(msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,106 @@
+// Fused AdamW over the flat fp32 parameter buffer for gfx950 (one launch for all 150M+ params).
+//
+// Replaces torch.optim.AdamW(model.parameters(), lr) .step() (src/main.py:68,155) — the
+// single-tensor algorithm, in its arithmetic order:
+//   p *= 1 - lr·wd;  m = m + (1-β1)(g - m)  (lerp);  v = β2·v + (1-β2)·g·g  (addcmul)
+//   p += -step_size · m / (sqrt(v)/bc2_sqrt + eps)           (addcdiv)
+// and refreshes the bf16 shadow copy the GEMMs read, in the same pass (HBM-bound: 30 B/param).
+#include "common.h"
+
+namespace ergm {
+
+__global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                                                    float4* __restrict__ m, float4* __restrict__ v,
+                                                    bf16x4* __restrict__ pb, size_t n4, float decay, float one_m_b1,
+                                                    float b2, float one_m_b2, float eps, float step_size,
+                                                    float bc2_sqrt) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        float* P = reinterpret_cast<float*>(&pp);
+        float* G = reinterpret_cast<float*>(&gg);
+        float* Mv = reinterpret_cast<float*>(&mm);
+        float* Vv = reinterpret_cast<float*>(&vv);
+        bf16x4 ob;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float x = P[j] * decay;
+            float mj = Mv[j] + one_m_b1 * (G[j] - Mv[j]);
+            float vj = Vv[j] * b2 + one_m_b2 * (G[j] * G[j]);
+            float denom = sqrtf(vj) / bc2_sqrt + eps;
+            x = x + (-step_size) * (mj / denom);
+            P[j] = x;
+            Mv[j] = mj;
+            Vv[j] = vj;
+            ob[j] = f2bf(x);
+        }
+        p[i] = pp;
+        m[i] = mm;
+        v[i] = vv;
+        if (pb) pb[i] = ob;
+    }
+}
+
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float4* __restrict__ src, bf16x4* __restrict__ dst,
+                                                        size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        float4 x = src[i];
+        bf16x4 o;
+        o[0] = f2bf(x.x); o[1] = f2bf(x.y); o[2] = f2bf(x.z); o[3] = f2bf(x.w);
+        dst[i] = o;
+    }
+}
+
+__global__ __launch_bounds__(256) void axpy_kernel(const float4* __restrict__ x, float4* __restrict__ y, size_t n4,
+                                                   float alpha) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        float4 a = x[i], b = y[i];
+        b.x += alpha * a.x; b.y += alpha * a.y; b.z += alpha * a.z; b.w += alpha * a.w;
+        y[i] = b;
+    }
+}
+
+static unsigned grid_for(size_t n4) {
+    size_t blocks = (n4 + 255) / 256;
+    return (unsigned)(blocks < 8192 ? (blocks ? blocks : 1) : 8192);
+}
+
+}  // namespace ergm
+
+using namespace ergm;
+
+extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
+                               float beta1, float beta2, float eps, float weight_decay, float step_size,
+                               float bc2_sqrt, void* stream) {
+    ERGM_CHECK_ARG(p && g && m && v, "adamw: null argument");
+    ERGM_CHECK_ARG(n % 4 == 0, "adamw: n must be a multiple of 4");
+    ERGM_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), "adamw: 16-byte alignment");
+    ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw: bf16 copy alignment");
+    size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    // the scalar products torch forms in double and rounds once when applied to fp32 tensors
+    float decay = (float)(1.0 - (double)lr * (double)weight_decay);
+    float one_m_b1 = (float)(1.0 - (double)beta1);
+    float one_m_b2 = (float)(1.0 - (double)beta2);
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2, one_m_b2, eps, step_size,
+                       bc2_sqrt);
+    return check_launch("adamw");
+}
+
+extern "C" int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream) {
+    ERGM_CHECK_ARG(src && dst && n % 4 == 0, "cast_bf16: bad argument");
+    size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)src,
+                       (bf16x4*)dst, n4);
+    return check_launch("cast_bf16");
+}
+
+extern "C" int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* stream) {
+    ERGM_CHECK_ARG(x && y && n % 4 == 0, "axpy: bad argument");
+    size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)x, (float4*)y,
+                       n4, alpha);
+    return check_launch("axpy");
+}

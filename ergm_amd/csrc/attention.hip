@@ -1,0 +1,437 @@
+// Fused multi-head attention (head_dim 64) forward/backward for gfx950.
+//
+// Replaces GPT2Attention._attn (src/model.py:119-148): W = QKᵀ / sqrt(d); causal
+// where(tril, W, finfo.min) for self-attention; additive all-zero encoder mask for the cross path
+// (src/model.py:484-489, elided); softmax; O = W·V — and its autograd backward.  _split_heads /
+// _merge_heads (src/model.py:190-198) are folded into addressing: Q/K/V/O are token-major
+// [b*S + s][h*64 + d] slices of the Conv1D outputs.
+//
+// Forward (flash-style, online softmax): one workgroup = 4 waves = 64 queries of one (b, h); each
+// wave owns 16 queries.  Scores are computed SWAPPED, Sᵀ = K·Qᵀ (v_mfma_f32_16x16x32_bf16), so a
+// lane holds 16 keys of ONE query: row max/sum are lane-local + two xor-shuffles.  The output is also
+// kept transposed, Oᵀ = Vᵀ·Pᵀ: P feeds the MFMA B operand straight from registers (k-order
+// permuted identically on both operands) and Vᵀ comes from the LDS V tile by ds_read_b64_tr_b16.
+// Backward: dK/dV kernel (workgroup = 64 keys, loops over query tiles, P recomputed from the
+// forward LSE) + dQ kernel (workgroup = 64 queries, loops over key tiles); no atomics, deterministic.
+#include "common.h"
+
+namespace ergm {
+
+constexpr int AT_D = 64;       // head dim
+constexpr int AT_T = 64;       // tile rows (queries or keys)
+constexpr int AT_TILE_BYTES = AT_T * AT_D * 2;  // 8 KiB
+
+// 64x64 bf16 tile in LDS, 128-B rows, 16-B chunk c of row r stored at chunk c ^ (r & 7):
+// conflict-free for both ds_read_b128 row reads and the ds_read_b64_tr_b16 reads below.
+__device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+// Stage rows [row0, row0+64) of a token-major tensor (row stride ld, head column offset col0).
+__device__ __forceinline__ void stage_tile(char* lds, const __bf16* base, int ld, int row0, int nrows, int col0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int c = threadIdx.x + i * 256;
+        int r = c >> 3, ch = c & 7;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (row0 + r < nrows) v = *reinterpret_cast<const uint4*>(base + (size_t)(row0 + r) * ld + col0 + ch * 8);
+        *reinterpret_cast<uint4*>(lds + tile_off(r, ch)) = v;
+    }
+}
+
+// Row-read operand fragment (16x16x32): lane l gets X[row0 + (l&15)][32ks + 8(l>>4) + j].
+__device__ __forceinline__ bf16x8 row_frag(const char* lds, int row0, int ks) {
+    const int lane = threadIdx.x & 63;
+    int row = row0 + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(lds + tile_off(row, ks * 4 + (lane >> 4)));
+}
+
+// Transposed operand fragment over 32 tile rows starting at krow0 (the MFMA k dim) and 16 columns
+// starting at col0 (the MFMA m dim): lane l (g = l>>4, i = l&15) gets element j =
+//   X[krow0 + 4g + j][col0 + i]        (j < 4)
+//   X[krow0 + 16 + 4g + j-4][col0 + i] (j >= 4)
+// — the same permuted k order as the P/dS register fragments (pack_p).
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int krow0, int col0) {
+    const int lane = threadIdx.x & 63;
+    const int i = lane & 15, g = lane >> 4;
+    const int col = col0 + 4 * (i & 3);
+    const int ch = col >> 3, sub = (col & 7) * 2;
+    const int r1 = krow0 + 4 * g + (i >> 2), r2 = r1 + 16;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + tile_off(r1, ch) + sub));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + tile_off(r2, ch) + sub));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// Register fragment holding rows [16*(2s)+4g .. +3] and [16*(2s+1)+4g .. +3] of a 16x16 accumulator
+// pair (accumulator row = (l>>4)*4 + r), i.e. the k order tr_frag uses.
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+    bf16x8 r;
+    r[0] = f2bf(a[0]); r[1] = f2bf(a[1]); r[2] = f2bf(a[2]); r[3] = f2bf(a[3]);
+    r[4] = f2bf(b[0]); r[5] = f2bf(b[1]); r[6] = f2bf(b[2]); r[7] = f2bf(b[3]);
+    return r;
+}
+
+__device__ __forceinline__ bf16x8 load_frag_global(const __bf16* base, int ld, int row, int nrows, int col) {
+    if (row < nrows) return *reinterpret_cast<const bf16x8*>(base + (size_t)row * ld + col);
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
+    return z;
+}
+
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+struct AttnArgs {
+    const __bf16 *q, *k, *v, *o, *dout;
+    __bf16 *out, *dq, *dk, *dv;
+    float *lse, *delta;
+    int B, H, Sq, Sk;
+    int ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
+    float scale;
+};
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) char sK[AT_TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char sV[AT_TILE_BYTES];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int qblk = blockIdx.x * AT_T;
+    const int q = qblk + wave * 16 + i16;  // this lane's query
+    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
+    const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
+    const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
+
+    // Qᵀ as the B operand: lane l needs Q[q][32ks + 8g + j]
+    bf16x8 qf[2];
+    qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
+    qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
+
+    f32x4 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+
+    int nkt = (a.Sk + AT_T - 1) / AT_T;
+    if (CAUSAL) {
+        int qlast = min(a.Sq, qblk + AT_T) - 1;
+        nkt = min(nkt, qlast / AT_T + 1);
+    }
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int key0 = kt * AT_T;
+        __syncthreads();
+        stage_tile(sK, Kb, a.ldk, key0, a.Sk, 0);
+        stage_tile(sV, Vb, a.ldv, key0, a.Sk, 0);
+        __syncthreads();
+        f32x4 s[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            s[kb] = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s[kb]);
+            s[kb] = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s[kb]);
+        }
+        // s[kb][r] = score(key = key0 + kb*16 + 4g + r, query q)
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int key = key0 + kb * 16 + 4 * g + r;
+                float x = s[kb][r] * a.scale;
+                bool masked = key >= a.Sk || (CAUSAL && key > q);
+                x = masked ? -INFINITY : x;
+                s[kb][r] = x;
+                mx = fmaxf(mx, x);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx);
+        const float muse = mnew == -INFINITY ? 0.f : mnew;
+        const float alpha = __expf(m - muse);
+        float rs = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float p = __expf(s[kb][r] - muse);
+                s[kb][r] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        m = mnew;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] *= alpha;
+        // Oᵀ[d][q] += Σ_key V[key][d] P[q][key]
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            bf16x8 pb = pack_p(s[2 * half], s[2 * half + 1]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) o[d] = MFMA16(tr_frag(sV, 32 * half, d * 16), pb, o[d]);
+        }
+    }
+    if (q < a.Sq) {
+        const float inv = l > 0.f ? 1.0f / l : 0.f;
+        __bf16* Ob = a.out + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            bf16x4 w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = f2bf(o[d][r] * inv);
+            *reinterpret_cast<bf16x4*>(Ob + d * 16 + 4 * g) = w;
+        }
+        if (g == 0) a.lse[((size_t)b * a.H + h) * a.Sq + q] = m + logf(l);
+    }
+}
+
+// delta[b,h,q] = Σ_d dO·O
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
+    const size_t n = (size_t)a.B * a.Sq * a.H;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int h = (int)(i % a.H);
+    size_t tok = i / a.H;  // b*Sq + q
+    const __bf16* dO = a.dout + tok * a.lddo + h * AT_D;
+    const __bf16* O = a.o + tok * a.ldo + h * AT_D;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < AT_D; c += 8) {
+        bf16x8 x = *reinterpret_cast<const bf16x8*>(dO + c);
+        bf16x8 y = *reinterpret_cast<const bf16x8*>(O + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += bf2f(x[j]) * bf2f(y[j]);
+    }
+    int b = (int)(tok / a.Sq), q = (int)(tok % a.Sq);
+    a.delta[((size_t)b * a.H + h) * a.Sq + q] = s;
+}
+
+// dK, dV: workgroup = 64 keys of one (b, h), each wave 16 keys; loop over query tiles.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) char sQ[AT_TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char sdO[AT_TILE_BYTES];
+    __shared__ float sL[AT_T], sD[AT_T];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int kblk = blockIdx.x * AT_T;
+    const int key = kblk + wave * 16 + i16;  // this lane's key (MFMA n index)
+    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
+    const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
+    const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
+    const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
+    const float* lse = a.lse + ((size_t)b * a.H + h) * a.Sq;
+    const float* dl = a.delta + ((size_t)b * a.H + h) * a.Sq;
+
+    // Kᵀ / Vᵀ as B operands: lane l needs K[key][32ks + 8g + j]
+    bf16x8 kf[2], vf[2];
+    kf[0] = load_frag_global(Kb, a.ldk, key, a.Sk, 8 * g);
+    kf[1] = load_frag_global(Kb, a.ldk, key, a.Sk, 32 + 8 * g);
+    vf[0] = load_frag_global(Vb, a.ldv, key, a.Sk, 8 * g);
+    vf[1] = load_frag_global(Vb, a.ldv, key, a.Sk, 32 + 8 * g);
+
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int nqt = (a.Sq + AT_T - 1) / AT_T;
+    const int qt0 = CAUSAL ? kblk / AT_T : 0;
+    for (int qt = qt0; qt < nqt; ++qt) {
+        const int q0 = qt * AT_T;
+        __syncthreads();
+        stage_tile(sQ, Qb, a.ldq, q0, a.Sq, 0);
+        stage_tile(sdO, dOb, a.lddo, q0, a.Sq, 0);
+        if (threadIdx.x < AT_T) {
+            int qq = q0 + threadIdx.x;
+            sL[threadIdx.x] = qq < a.Sq ? lse[qq] : 0.f;
+            sD[threadIdx.x] = qq < a.Sq ? dl[qq] : 0.f;
+        }
+        __syncthreads();
+        f32x4 p[4], ds[4];
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb) {
+            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+            s = MFMA16(row_frag(sQ, qb * 16, 0), kf[0], s);
+            s = MFMA16(row_frag(sQ, qb * 16, 1), kf[1], s);
+            f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
+            dp = MFMA16(row_frag(sdO, qb * 16, 0), vf[0], dp);
+            dp = MFMA16(row_frag(sdO, qb * 16, 1), vf[1], dp);
+            // element r: query q0 + qb*16 + 4g + r, key `key`
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int ql = qb * 16 + 4 * g + r;
+                int qq = q0 + ql;
+                bool masked = qq >= a.Sq || key >= a.Sk || (CAUSAL && key > qq);
+                float pv = masked ? 0.f : __expf(s[r] * a.scale - sL[ql]);
+                p[qb][r] = pv;
+                ds[qb][r] = pv * (dp[r] - sD[ql]);
+            }
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            bf16x8 pb = pack_p(p[2 * half], p[2 * half + 1]);
+            bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                dv[d] = MFMA16(tr_frag(sdO, 32 * half, d * 16), pb, dv[d]);
+                dk[d] = MFMA16(tr_frag(sQ, 32 * half, d * 16), sb, dk[d]);
+            }
+        }
+    }
+    if (key < a.Sk) {
+        size_t tok = (size_t)b * a.Sk + key;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            bf16x4 wk, wv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                wk[r] = f2bf(dk[d][r] * a.scale);
+                wv[r] = f2bf(dv[d][r]);
+            }
+            *reinterpret_cast<bf16x4*>(a.dk + tok * a.lddk + h * AT_D + d * 16 + 4 * g) = wk;
+            *reinterpret_cast<bf16x4*>(a.dv + tok * a.lddv + h * AT_D + d * 16 + 4 * g) = wv;
+        }
+    }
+}
+
+// dQ: workgroup = 64 queries, each wave 16 queries; loop over key tiles.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) char sK[AT_TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char sV[AT_TILE_BYTES];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int qblk = blockIdx.x * AT_T;
+    const int q = qblk + wave * 16 + i16;
+    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
+    const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
+    const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
+    const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
+    const size_t sidx = ((size_t)b * a.H + h) * a.Sq + q;
+    const float lq = q < a.Sq ? a.lse[sidx] : 0.f;
+    const float dq_delta = q < a.Sq ? a.delta[sidx] : 0.f;
+
+    bf16x8 qf[2], dof[2];
+    qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
+    qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
+    dof[0] = load_frag_global(dOb, a.lddo, q, a.Sq, 8 * g);
+    dof[1] = load_frag_global(dOb, a.lddo, q, a.Sq, 32 + 8 * g);
+
+    f32x4 dq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int nkt = (a.Sk + AT_T - 1) / AT_T;
+    if (CAUSAL) {
+        int qlast = min(a.Sq, qblk + AT_T) - 1;
+        nkt = min(nkt, qlast / AT_T + 1);
+    }
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int key0 = kt * AT_T;
+        __syncthreads();
+        stage_tile(sK, Kb, a.ldk, key0, a.Sk, 0);
+        stage_tile(sV, Vb, a.ldv, key0, a.Sk, 0);
+        __syncthreads();
+        f32x4 ds[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+            s = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s);
+            s = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s);
+            f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
+            dp = MFMA16(row_frag(sV, kb * 16, 0), dof[0], dp);
+            dp = MFMA16(row_frag(sV, kb * 16, 1), dof[1], dp);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int key = key0 + kb * 16 + 4 * g + r;
+                bool masked = key >= a.Sk || q >= a.Sq || (CAUSAL && key > q);
+                float pv = masked ? 0.f : __expf(s[r] * a.scale - lq);
+                ds[kb][r] = pv * (dp[r] - dq_delta);
+            }
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) dq[d] = MFMA16(tr_frag(sK, 32 * half, d * 16), sb, dq[d]);
+        }
+    }
+    if (q < a.Sq) {
+        __bf16* out = a.dq + ((size_t)b * a.Sq + q) * a.lddq + h * AT_D;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            bf16x4 w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = f2bf(dq[d][r] * a.scale);
+            *reinterpret_cast<bf16x4*>(out + d * 16 + 4 * g) = w;
+        }
+    }
+}
+
+static int check_common(const void* q, const void* k, const void* v, int B, int H, int Sq, int Sk, int ldq, int ldk,
+                        int ldv, int causal) {
+    ERGM_CHECK_ARG(q && k && v, "attn: null argument");
+    ERGM_CHECK_ARG(B > 0 && H > 0 && Sq > 0 && Sk > 0, "attn: bad shape");
+    ERGM_CHECK_ARG(!causal || Sq == Sk, "attn: causal needs Sq == Sk");
+    ERGM_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "attn: leading dims must be multiples of 8");
+    ERGM_CHECK_ARG(ldq >= H * AT_D && ldk >= H * AT_D && ldv >= H * AT_D, "attn: leading dim < H*64");
+    ERGM_CHECK_ARG(aligned16(q) && aligned16(k) && aligned16(v), "attn: pointers must be 16-byte aligned");
+    return ERGM_OK;
+}
+
+}  // namespace ergm
+
+using namespace ergm;
+
+extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
+                             int Sk, int ldq, int ldk, int ldv, int ldo, int causal, void* stream) {
+    ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
+    ERGM_CHECK_ARG(o && lse && ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd: bad output");
+    AttnArgs a{};
+    a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+    a.out = (__bf16*)o; a.lse = lse;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+    a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
+    a.scale = 0.125f;  // 1/sqrt(64): exact, so x*scale == x / 8.0 (src/model.py:122-125)
+    dim3 grid(cdiv(Sq, AT_T), H, B);
+    hipStream_t s = as_stream(stream);
+    if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, a);
+    return check_launch("attn_fwd");
+}
+
+extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                             const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
+                             int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
+                             int causal, void* stream) {
+    ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
+    ERGM_CHECK_ARG(o && dout && lse && delta && dq && dk && dv, "attn_bwd: null argument");
+    ERGM_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 4 == 0 && lddk % 4 == 0 && lddv % 4 == 0,
+                   "attn_bwd: bad leading dims");
+    ERGM_CHECK_ARG(aligned16(o) && aligned16(dout), "attn_bwd: O/dO must be 16-byte aligned");
+    AttnArgs a{};
+    a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+    a.o = (const __bf16*)o; a.dout = (const __bf16*)dout;
+    a.dq = (__bf16*)dq; a.dk = (__bf16*)dk; a.dv = (__bf16*)dv;
+    a.lse = (float*)lse; a.delta = delta;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+    a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo;
+    a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
+    a.scale = 0.125f;
+    hipStream_t s = as_stream(stream);
+    size_t n = (size_t)B * Sq * H;
+    hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+    dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
+    if (causal) {
+        hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, gk, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, gq, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(attn_bwd_dkv_kernel<false>, gk, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, gq, dim3(256), 0, s, a);
+    }
+    return check_launch("attn_bwd");
+}

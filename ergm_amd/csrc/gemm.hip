@@ -1,0 +1,394 @@
+// bf16 MFMA GEMM for gfx950 (CDNA4): every Conv1D / Linear contraction of the ERGM training step.
+//
+// Replaces transformers Conv1D.forward (addmm(b, x, W[in,out])) used at src/model.py:95-99,257-258,
+// the tied lm_head nn.Linear (src/model.py:605,698) and their autograd backward GEMMs.
+//
+// C[M][N] = epilogue(alpha * Σ_k A(m,k) B(k,n)), A/B bf16, fp32 accumulate.
+//   A storage: MK = A[m][k] (k contiguous) or KM = A[k][m]      (KM: weight-gradient GEMMs Xᵀ·dY)
+//   B storage: NK = B[n][k] (Linear weight) or KN = B[k][n]    (Conv1D weight [in,out])
+// Tiles of BM×BN×64 staged global→registers→LDS (double buffered, one barrier per K-step);
+// 4 waves (2×2), each owning (BM/2)×(BN/2) as 16×16 MFMA tiles (v_mfma_f32_16x16x32_bf16).
+// k-contiguous tiles are read row-wise with ds_read_b128 (16-B chunk XOR row&7 swizzle);
+// m/n-contiguous tiles are read column-wise with ds_read_b64_tr_b16 (CDNA4 transpose read) under a
+// row-dependent chunk XOR that keeps each 32-lane half conflict-free.
+#include "common.h"
+
+namespace ergm {
+
+constexpr int GEMM_BK = 64;
+constexpr int GEMM_THREADS = 256;
+
+struct GemmArgs {
+    const __bf16* A;
+    const __bf16* B;
+    void* C;
+    int M, N, K;
+    int lda, ldb, ldc;
+    float alpha;
+    const float* alpha_dev;
+    const float* bias;
+    const void* aux;
+    int ld_aux;
+    void* aux_out;
+    int ld_aux_out;
+    int tiles_m, tiles_n;
+    int sweep_m;        // 1: consecutive tile ids walk M (B panel reused), 0: walk N
+    int k_per_split;    // K range per blockIdx.z (multiple of 64)
+    float* slab;        // split-K partials [z][M][N] (f32) or nullptr
+};
+
+// XOR swizzles (chunk = 16 bytes).
+__device__ __forceinline__ int swz_row(int row) { return row & 7; }  // 128-B rows, row reads
+// transposed-read tiles: rows {8g+q} (g=0,1; q=0..3) of a half-wave must hit distinct slots
+__device__ __forceinline__ int swz_tr16(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }        // 256-B rows
+__device__ __forceinline__ int swz_tr8(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }  // 128-B rows
+
+template <int ROWS, bool TRANS>
+struct TileLoader {
+    // ROWS = tile extent along M (A) or N (B).  !TRANS: tile [ROWS][64] (k contiguous);
+    // TRANS: tile [64][ROWS] (ROWS contiguous).
+    static constexpr int CHUNKS = ROWS * GEMM_BK / 8;       // 16-B chunks per tile
+    static constexpr int PER_THREAD = CHUNKS / GEMM_THREADS;
+    static constexpr int CPR = TRANS ? ROWS / 8 : 8;         // chunks per LDS row
+    static constexpr int ROW_BYTES = CPR * 16;
+    static_assert(PER_THREAD >= 1, "tile too small");
+
+    uint4 regs[PER_THREAD];
+
+    // global → registers. base: operand pointer, ld: leading dim, r0: tile origin along ROWS dim,
+    // k0: K origin, R: extent along ROWS dim (M or N), K: contraction extent (k_end).
+    __device__ __forceinline__ void load(const __bf16* base, int ld, int r0, int k0, int R, int Kend) {
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i) {
+            int c = threadIdx.x + i * GEMM_THREADS;
+            int lrow = c / CPR, lc = c % CPR;
+            bool ok;
+            const __bf16* p;
+            if (!TRANS) {  // row = r, chunk along k
+                int r = r0 + lrow, k = k0 + lc * 8;
+                ok = (r < R) && (k < Kend);
+                p = base + (size_t)r * ld + k;
+            } else {       // row = k, chunk along r
+                int k = k0 + lrow, r = r0 + lc * 8;
+                ok = (k < Kend) && (r < R);
+                p = base + (size_t)k * ld + r;
+            }
+            regs[i] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i) {
+            int c = threadIdx.x + i * GEMM_THREADS;
+            int lrow = c / CPR, lc = c % CPR;
+            int pc;
+            if (!TRANS) pc = lc ^ swz_row(lrow);
+            else pc = lc ^ (CPR == 16 ? swz_tr16(lrow) : swz_tr8(lrow));
+            *reinterpret_cast<uint4*>(lds + lrow * ROW_BYTES + pc * 16) = regs[i];
+        }
+    }
+    // MFMA 16x16x32 operand fragment for the 16 rows starting at `ro` (tile-relative), k-step ks.
+    // Lane l gets element j = X[ro + (l&15)][32ks + 8(l>>4) + j].
+    __device__ __forceinline__ bf16x8 frag(const char* lds, int ro, int ks) const {
+        const int lane = threadIdx.x & 63;
+        if (!TRANS) {
+            int row = ro + (lane & 15);
+            int ch = ks * 4 + (lane >> 4);
+            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ swz_row(row)) << 4));
+        } else {
+            int i16 = lane & 15, g = lane >> 4;
+            int k = ks * 32 + 8 * g + (i16 >> 2);
+            int col = ro + 4 * (i16 & 3);
+            int ch = col >> 3;
+            int sub = (col & 7) * 2;  // byte offset within chunk (0 or 8)
+            int s1 = CPR == 16 ? swz_tr16(k) : swz_tr8(k);
+            int s2 = CPR == 16 ? swz_tr16(k + 4) : swz_tr8(k + 4);
+            const char* p1 = lds + k * ROW_BYTES + ((ch ^ s1) << 4) + sub;
+            const char* p2 = lds + (k + 4) * ROW_BYTES + ((ch ^ s2) << 4) + sub;
+            s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p1));
+            s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p2));
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            return __builtin_bit_cast(bf16x8, r);
+        }
+    }
+};
+
+template <int EPI, bool OUT_BF16>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, float v) {
+    if (EPI == ERGM_EPI_BIAS || EPI == ERGM_EPI_BIAS_GELU || EPI == ERGM_EPI_BIAS_RESID) {
+        if (a.bias) v += a.bias[n];
+    }
+    if (EPI == ERGM_EPI_BIAS_GELU) {
+        __bf16 pre = f2bf(v);
+        reinterpret_cast<__bf16*>(a.aux_out)[(size_t)m * a.ld_aux_out + n] = pre;
+        v = gelu_new(v);
+    } else if (EPI == ERGM_EPI_BIAS_RESID) {
+        v += reinterpret_cast<const float*>(a.aux)[(size_t)m * a.ld_aux + n];
+    } else if (EPI == ERGM_EPI_GELU_BWD) {
+        float x = bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);
+        v *= gelu_new_grad(x);
+    }
+    size_t idx = (size_t)m * a.ldc + n;
+    if (OUT_BF16) {
+        reinterpret_cast<__bf16*>(a.C)[idx] = f2bf(v);
+    } else {
+        float* c = reinterpret_cast<float*>(a.C);
+        if (EPI == ERGM_EPI_ACCUM) v += c[idx];
+        c[idx] = v;
+    }
+}
+
+// bijective XCD-grouping remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous range.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int NX = 8;
+    if (nwg < NX) return bid;
+    int xcd = bid % NX, idx = bid / NX;
+    int q = nwg / NX, r = nwg % NX;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + idx;
+}
+
+template <int BM, int BN, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int STAGE = A_BYTES + B_BYTES;
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int id = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = blockIdx.z * a.k_per_split;
+    const int kend = min(a.K, kbeg + a.k_per_split);
+    const int nk = (kend - kbeg + GEMM_BK - 1) / GEMM_BK;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+
+    TileLoader<BM, A_KM> la;
+    TileLoader<BN, B_KN> lb;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) {
+        la.load(a.A, a.lda, m0, kbeg, a.M, kend);
+        lb.load(a.B, a.ldb, n0, kbeg, a.N, kend);
+        la.store(smem);
+        lb.store(smem + A_BYTES);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            la.load(a.A, a.lda, m0, kbeg + (kt + 1) * GEMM_BK, a.M, kend);
+            lb.load(a.B, a.ldb, n0, kbeg + (kt + 1) * GEMM_BK, a.N, kend);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fa[FM], fb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) fa[i] = la.frag(smem + cur * STAGE, wm * WM + i * 16, ks);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fb[j] = lb.frag(smem + cur * STAGE + A_BYTES, wn * WN + j * 16, ks);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) {
+            la.store(smem + (cur ^ 1) * STAGE);
+            lb.store(smem + (cur ^ 1) * STAGE + A_BYTES);
+        }
+        __syncthreads();
+    }
+
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    const int rbase = m0 + wm * WM + (lane >> 4) * 4;
+    const int cbase = n0 + wn * WN + (lane & 15);
+    if (a.slab) {
+        float* slab = a.slab + (size_t)blockIdx.z * a.M * a.N;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int m = rbase + i * 16 + r, n = cbase + j * 16;
+                    if (m < a.M && n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][r];
+                }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = rbase + i * 16 + r, n = cbase + j * 16;
+                if (m < a.M && n < a.N) epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
+            }
+}
+
+// split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
+template <int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int splits) {
+    size_t total = (size_t)a.M * a.N;
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int z = 0; z < splits; ++z) s += a.slab[(size_t)z * total + i];
+        int m = (int)(i / a.N), n = (int)(i % a.N);
+        epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * s);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host dispatch
+// ------------------------------------------------------------------------------------------
+struct GemmPlan {
+    int bm, bn, split, kps;
+};
+
+static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
+    GemmPlan p;
+    const int M = d->M, N = d->N, K = d->K;
+    long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
+    long t64 = (long)cdiv(M, 64) * cdiv(N, 64);
+    bool can128 = !(d->a_layout == ERGM_KM && M % 8) && !(d->b_layout == ERGM_KN && N % 8);
+    if (can128 && t128 >= 240) { p.bm = 128; p.bn = 128; }
+    else { p.bm = 64; p.bn = 64; }
+    long tiles = (long)cdiv(M, p.bm) * cdiv(N, p.bn);
+    int split = 1;
+    if (d->split_k > 1) split = d->split_k;
+    else if (d->split_k == 0 && tiles < 200 && K >= 1024) {
+        split = (int)((400 + tiles - 1) / tiles);
+        int maxs = K / 512;
+        if (split > maxs) split = maxs;
+        if (split < 1) split = 1;
+    }
+    int kps = cdiv(cdiv(K, split), GEMM_BK) * GEMM_BK;
+    split = cdiv(K, kps);
+    p.split = split;
+    p.kps = kps;
+    return p;
+}
+
+template <int BM, int BN, bool AKM, bool BKN, int EPI, bool OB>
+static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
+    constexpr size_t lds = 2 * (BM + BN) * GEMM_BK * 2;
+    dim3 grid(a.tiles_m * a.tiles_n, 1, split);
+    if (split > 1) {
+        // raw partials: epilogue handled by splitk_reduce_kernel
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, EPI, OB>), grid, dim3(GEMM_THREADS), lds, s, a);
+    }
+}
+
+template <int EPI, bool OB>
+static void launch_layout(const GemmArgs& a, const GemmPlan& p, int al, int bl, hipStream_t s) {
+#define ERGM_GEMM_LAYOUTS(BM, BN)                                                      \
+    if (al == ERGM_MK && bl == ERGM_NK) launch_t<BM, BN, false, false, EPI, OB>(a, p.split, s); \
+    else if (al == ERGM_MK && bl == ERGM_KN) launch_t<BM, BN, false, true, EPI, OB>(a, p.split, s); \
+    else if (al == ERGM_KM && bl == ERGM_NK) launch_t<BM, BN, true, false, EPI, OB>(a, p.split, s); \
+    else launch_t<BM, BN, true, true, EPI, OB>(a, p.split, s);
+    if (p.bm == 128) { ERGM_GEMM_LAYOUTS(128, 128) }
+    else { ERGM_GEMM_LAYOUTS(64, 64) }
+#undef ERGM_GEMM_LAYOUTS
+}
+
+template <int EPI, bool OB>
+static void launch_reduce(const GemmArgs& a, int split, hipStream_t s) {
+    size_t total = (size_t)a.M * a.N;
+    int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL((splitk_reduce_kernel<EPI, OB>), dim3(blocks), dim3(256), 0, s, a, split);
+}
+
+}  // namespace ergm
+
+using namespace ergm;
+
+extern "C" size_t ergm_gemm_workspace_size(const ergm_gemm_desc* d) {
+    if (!d) return 0;
+    GemmPlan p = plan_gemm(d);
+    if (p.split <= 1) return 0;
+    return (size_t)p.split * d->M * d->N * sizeof(float);
+}
+
+extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, void* C, void* ws,
+                         size_t ws_bytes, void* stream) {
+    ERGM_CHECK_ARG(d && A && B && C, "ergm_gemm: null argument");
+    ERGM_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "ergm_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
+    ERGM_CHECK_ARG(d->K % 8 == 0, "ergm_gemm: K=%d must be a multiple of 8", d->K);
+    ERGM_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "ergm_gemm: lda/ldb must be multiples of 8 elements");
+    ERGM_CHECK_ARG(aligned16(A) && aligned16(B), "ergm_gemm: A/B must be 16-byte aligned");
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK || d->a_layout == ERGM_KM, "ergm_gemm: bad a_layout");
+    ERGM_CHECK_ARG(d->b_layout == ERGM_NK || d->b_layout == ERGM_KN, "ergm_gemm: bad b_layout");
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK ? d->lda >= d->K : d->lda >= d->M, "ergm_gemm: lda too small");
+    ERGM_CHECK_ARG(d->b_layout == ERGM_NK ? d->ldb >= d->K : d->ldb >= d->N, "ergm_gemm: ldb too small");
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK || d->M % 8 == 0, "ergm_gemm: KM layout needs M %% 8 == 0");
+    ERGM_CHECK_ARG(d->b_layout == ERGM_NK || d->N % 8 == 0, "ergm_gemm: KN layout needs N %% 8 == 0");
+    ERGM_CHECK_ARG(d->ldc >= d->N, "ergm_gemm: ldc < N");
+    ERGM_CHECK_ARG(d->c_dtype == ERGM_F32 || d->c_dtype == ERGM_BF16, "ergm_gemm: bad c_dtype");
+    int e = d->epilogue;
+    ERGM_CHECK_ARG(e >= ERGM_EPI_NONE && e <= ERGM_EPI_ACCUM, "ergm_gemm: bad epilogue %d", e);
+    ERGM_CHECK_ARG(!(e == ERGM_EPI_BIAS_RESID || e == ERGM_EPI_ACCUM) || d->c_dtype == ERGM_F32,
+                   "ergm_gemm: residual/accumulate epilogues need f32 C");
+    ERGM_CHECK_ARG(!(e == ERGM_EPI_BIAS_RESID || e == ERGM_EPI_GELU_BWD) || d->aux, "ergm_gemm: epilogue needs aux");
+    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || d->aux_out, "ergm_gemm: BIAS_GELU needs aux_out");
+
+    GemmPlan p = plan_gemm(d);
+    GemmArgs a;
+    a.A = reinterpret_cast<const __bf16*>(A);
+    a.B = reinterpret_cast<const __bf16*>(B);
+    a.C = C;
+    a.M = d->M; a.N = d->N; a.K = d->K;
+    a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+    a.alpha = d->alpha; a.alpha_dev = d->alpha_dev;
+    a.bias = d->bias; a.aux = d->aux; a.ld_aux = d->ld_aux;
+    a.aux_out = d->aux_out; a.ld_aux_out = d->ld_aux_out;
+    a.tiles_m = cdiv(d->M, p.bm); a.tiles_n = cdiv(d->N, p.bn);
+    // stream the larger operand once: walk along the dimension of the smaller operand
+    a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
+    a.k_per_split = p.kps;
+    a.slab = nullptr;
+    hipStream_t s = as_stream(stream);
+    if (p.split > 1) {
+        size_t need = (size_t)p.split * d->M * d->N * sizeof(float);
+        ERGM_CHECK_ARG(ws && ws_bytes >= need, "ergm_gemm: split-K %d needs %zu workspace bytes (got %zu)", p.split,
+                       need, ws_bytes);
+        a.slab = reinterpret_cast<float*>(ws);
+    }
+    const bool ob = d->c_dtype == ERGM_BF16;
+#define ERGM_EPI_CASE(E)                                                  \
+    case E:                                                               \
+        if (ob) launch_layout<E, true>(a, p, d->a_layout, d->b_layout, s); \
+        else launch_layout<E, false>(a, p, d->a_layout, d->b_layout, s);   \
+        if (p.split > 1) {                                                \
+            if (ob) launch_reduce<E, true>(a, p.split, s);                 \
+            else launch_reduce<E, false>(a, p.split, s);                   \
+        }                                                                 \
+        break;
+    switch (e) {
+        ERGM_EPI_CASE(ERGM_EPI_NONE)
+        ERGM_EPI_CASE(ERGM_EPI_BIAS)
+        ERGM_EPI_CASE(ERGM_EPI_BIAS_GELU)
+        ERGM_EPI_CASE(ERGM_EPI_BIAS_RESID)
+        ERGM_EPI_CASE(ERGM_EPI_GELU_BWD)
+        ERGM_EPI_CASE(ERGM_EPI_ACCUM)
+    }
+#undef ERGM_EPI_CASE
+    return check_launch("ergm_gemm");
+}

@@ -1,0 +1,433 @@
+// Native executor for the whole fused GPT-2 (ERGM) training step on gfx950.
+//
+// ergm_model_forward   = GPT2LMHeadModel.forward (src/model.py:654-737): embeddings + fusion
+//                        (:459-506), L × GPT2Block (:286-341: self-attn, cross-attn over caption
+//                        embeddings, MLP), ln_f (:578), tied LM head (:698), emotion head (:700-701),
+//                        LM + emotion CE (:704-713)
+// ergm_model_backward_* = loss.backward() (src/main.py:154) in three stages (head, per block, embed)
+//                        so a data-parallel caller can all-reduce finished gradient buckets while the
+//                        remaining blocks run.
+// One C call launches a whole stage (no per-op Python/ctypes overhead); every buffer is caller-owned.
+// Design points: the cross-attention K/V projection of the caption embeddings — the same
+// tensor in every block (src/model.py:521) — runs as ONE GEMM for all L blocks with the stacked
+// weights [E][L·2E]; its backward is likewise one dX GEMM (contraction over L·2E) and one dW GEMM.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "common.h"
+
+using namespace ergm;
+
+struct LayerActs {
+    __bf16 *ln1, *lnx, *ln2;
+    float *m1, *r1, *mx, *rx, *m2, *r2;
+    __bf16 *qkv, *ao, *xq, *xo, *pre, *act;
+    float *lse, *xlse;
+};
+
+struct ergm_model_plan {
+    ergm_model_dims d;
+    ergm_model_params p;
+    int T, L2E;
+    // activations
+    float** resid;  // 3L+1 residual-stream tensors [T][E] f32
+    std::vector<float*> resid_v;
+    std::vector<LayerActs> la;
+    __bf16 *cap, *kv_all, *lnf;
+    float *mf, *rf;
+    __bf16* dlogits;
+    float *row_loss, *emo_sum, *emo_tmp;
+    int* n_valid_local;
+    // backward scratch
+    float *dh, *dy, *dcap, *delta;
+    __bf16 *dh_b, *d_o, *dqkv, *dxq, *dkv_all, *dpre;
+    char* scratch;
+    size_t scratch_bytes;
+    // inputs
+    const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
+    const float *vis, *aud;
+    const int* n_valid;
+    int B_global;
+    bool have_fwd;
+    // dry-run sizing
+    bool dry;
+    size_t need;
+};
+
+namespace {
+
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <typename T>
+    T* take(size_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+// Lay out every activation buffer; returns bytes used (scratch excluded).
+size_t carve(ergm_model_plan* P, char* base) {
+    const ergm_model_dims& d = P->d;
+    const size_t T = (size_t)d.batch * d.seq, E = d.n_embd, F = d.n_inner, L = d.n_layer;
+    const size_t BHS = (size_t)d.batch * d.n_head * d.seq;
+    Carver c{base};
+    P->resid_v.assign(3 * L + 1, nullptr);
+    for (size_t i = 0; i < 3 * L + 1; ++i) P->resid_v[i] = c.take<float>(T * E);
+    P->la.assign(L, LayerActs{});
+    for (size_t l = 0; l < L; ++l) {
+        LayerActs& a = P->la[l];
+        a.ln1 = c.take<__bf16>(T * E); a.lnx = c.take<__bf16>(T * E); a.ln2 = c.take<__bf16>(T * E);
+        a.m1 = c.take<float>(T); a.r1 = c.take<float>(T); a.mx = c.take<float>(T);
+        a.rx = c.take<float>(T); a.m2 = c.take<float>(T); a.r2 = c.take<float>(T);
+        a.qkv = c.take<__bf16>(T * 3 * E); a.ao = c.take<__bf16>(T * E);
+        a.xq = c.take<__bf16>(T * E); a.xo = c.take<__bf16>(T * E);
+        a.pre = c.take<__bf16>(T * F); a.act = c.take<__bf16>(T * F);
+        a.lse = c.take<float>(BHS); a.xlse = c.take<float>(BHS);
+    }
+    P->cap = c.take<__bf16>(T * E);
+    P->kv_all = c.take<__bf16>(T * 2 * E * L);
+    P->lnf = c.take<__bf16>(T * E);
+    P->mf = c.take<float>(T); P->rf = c.take<float>(T);
+    P->dlogits = c.take<__bf16>(T * d.vocab_pad);
+    P->row_loss = c.take<float>(T);
+    P->emo_sum = c.take<float>(4);
+    P->emo_tmp = c.take<float>((size_t)d.batch * 7 + 4);
+    P->n_valid_local = c.take<int>(4);
+    P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
+    P->delta = c.take<float>(BHS);
+    P->dh_b = c.take<__bf16>(T * E); P->d_o = c.take<__bf16>(T * E);
+    P->dqkv = c.take<__bf16>(T * 3 * E); P->dxq = c.take<__bf16>(T * E);
+    P->dkv_all = c.take<__bf16>(T * 2 * E * L);
+    P->dpre = c.take<__bf16>(T * F);
+    P->scratch = c.take<char>(0);
+    P->resid = P->resid_v.data();
+    return c.off;
+}
+
+inline int ws_need(ergm_model_plan* P, size_t bytes) {
+    if (P->dry) {
+        P->need = std::max(P->need, bytes);
+        return ERGM_OK;
+    }
+    ERGM_CHECK_ARG(bytes <= P->scratch_bytes, "model: scratch %zu < %zu", P->scratch_bytes, bytes);
+    return ERGM_OK;
+}
+
+int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, int lda, int al, const void* B,
+         int ldb, int bl, void* C, int ldc, int cdt, int epi, const float* bias = nullptr, const void* aux = nullptr,
+         int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const float* alpha_dev = nullptr) {
+    ergm_gemm_desc g;
+    memset(&g, 0, sizeof(g));
+    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+    g.a_layout = al; g.b_layout = bl; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
+    g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
+    g.split_k = 0; g.alpha_dev = alpha_dev;
+    size_t w = ergm_gemm_workspace_size(&g);
+    ERGM_TRY(ws_need(P, w));
+    if (P->dry) return ERGM_OK;
+    return ergm_gemm(&g, A, B, C, P->scratch, P->scratch_bytes, s);
+}
+
+int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, int cols, int ldx, float* out) {
+    ERGM_TRY(ws_need(P, ergm_colsum_workspace_size(rows, cols)));
+    if (P->dry) return ERGM_OK;
+    return ergm_colsum(X, dt, rows, cols, ldx, out, 0, P->scratch, P->scratch_bytes, s);
+}
+
+int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
+           float* dgamma, float* dbeta) {
+    const int T = P->T, E = P->d.n_embd;
+    ERGM_TRY(ws_need(P, ergm_layernorm_bwd_workspace_size(T, E)));
+    if (P->dry) return ERGM_OK;
+    return ergm_layernorm_bwd(P->dy, x, mean, rstd, gamma, P->dh, P->dh_b, dgamma, dbeta, P->scratch, P->scratch_bytes,
+                              T, E, s);
+}
+
+inline const float* LF(const ergm_model_plan* P, int l, int t) {
+    return P->p.layer_f32 + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
+}
+inline const __bf16* LB(const ergm_model_plan* P, int l, int t) {
+    return reinterpret_cast<const __bf16*>(P->p.layer_b16) + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
+}
+inline float* LG(const ergm_model_plan* P, int l, int t) {
+    return P->p.g_layer + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
+}
+
+int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s);
+int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s);
+int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s);
+int do_backward_embed(ergm_model_plan* P, hipStream_t s);
+
+}  // namespace
+
+extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
+    if (!dims) return 0;
+    ergm_model_plan P;
+    P.d = *dims;
+    memset(&P.p, 0, sizeof(P.p));
+    P.T = dims->batch * dims->seq;
+    P.L2E = 2 * dims->n_embd * dims->n_layer;
+    size_t act = carve(&P, nullptr);
+    P.dry = true;
+    P.need = ergm_embed_bwd_workspace_size(P.T);
+    P.need = std::max(P.need, ergm_colsum_workspace_size(P.T, std::max(P.L2E, dims->n_inner)));
+    P.labels = P.emo_labels = nullptr;
+    do_forward(&P, nullptr, nullptr, nullptr, 1, nullptr);
+    do_backward_head(&P, nullptr, nullptr);
+    do_backward_layer(&P, 0, nullptr);
+    do_backward_embed(&P, nullptr);
+    return ((act + 255) & ~(size_t)255) + P.need + 256;
+}
+
+extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* ws,
+                                 size_t ws_bytes, ergm_model_plan** out) {
+    ERGM_CHECK_ARG(dims && params && ws && out, "model_create: null argument");
+    const ergm_model_dims& d = *dims;
+    ERGM_CHECK_ARG(d.n_embd > 0 && d.n_head > 0 && d.n_embd == 64 * d.n_head,
+                   "model_create: head_dim must be 64 (n_embd=%d n_head=%d)", d.n_embd, d.n_head);
+    ERGM_CHECK_ARG(d.n_embd % 64 == 0 && d.n_embd <= 1024, "model_create: n_embd=%d unsupported", d.n_embd);
+    ERGM_CHECK_ARG(d.n_inner % 64 == 0, "model_create: n_inner must be a multiple of 64");
+    ERGM_CHECK_ARG(d.vocab > 0 && d.vocab_pad >= d.vocab && d.vocab_pad % 64 == 0, "model_create: bad vocab_pad");
+    ERGM_CHECK_ARG(d.batch > 0 && d.seq >= 2 && d.seq <= d.n_positions, "model_create: bad batch/seq");
+    ERGM_CHECK_ARG((d.batch * d.seq) % 8 == 0, "model_create: B*S must be a multiple of 8");
+    ERGM_CHECK_ARG(d.n_layer > 0, "model_create: n_layer must be > 0");
+    size_t need = ergm_model_workspace_size(dims);
+    ERGM_CHECK_ARG(ws_bytes >= need, "model_create: workspace %zu < %zu bytes", ws_bytes, need);
+    auto* P = new (std::nothrow) ergm_model_plan();
+    if (!P) return fail(ERGM_EINVAL, "model_create: out of host memory");
+    P->d = d;
+    P->p = *params;
+    P->T = d.batch * d.seq;
+    P->L2E = 2 * d.n_embd * d.n_layer;
+    size_t act = carve(P, reinterpret_cast<char*>(ws));
+    act = (act + 255) & ~(size_t)255;
+    P->scratch = reinterpret_cast<char*>(ws) + act;
+    P->scratch_bytes = ws_bytes - act;
+    P->dry = false;
+    P->need = 0;
+    P->have_fwd = false;
+    P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
+    P->vis = P->aud = nullptr;
+    P->n_valid = nullptr;
+    P->B_global = d.batch;
+    *out = P;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_destroy(ergm_model_plan* P) {
+    delete P;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_inputs(ergm_model_plan* P, const int64_t* ids, const int64_t* tt,
+                                     const int64_t* cap_ids, const float* vis, const float* aud,
+                                     const int64_t* labels, const int64_t* emotion_labels, const int* n_valid_global,
+                                     int B_global) {
+    ERGM_CHECK_ARG(P && ids && cap_ids, "model_set_inputs: input_ids and caption_ids are required");
+    ERGM_CHECK_ARG((vis == nullptr) == (aud == nullptr), "model_set_inputs: visual/audio features go together");
+    ERGM_CHECK_ARG(!vis || P->d.has_features, "model_set_inputs: plan built without features");
+    ERGM_CHECK_ARG(!labels || n_valid_global, "model_set_inputs: labels need n_valid_global");
+    P->ids = ids; P->tt = tt; P->cap_ids = cap_ids; P->vis = vis; P->aud = aud;
+    P->labels = labels; P->emo_labels = emotion_labels; P->n_valid = n_valid_global;
+    P->B_global = B_global > 0 ? B_global : P->d.batch;
+    return ERGM_OK;
+}
+
+namespace {
+int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s) {
+    const ergm_model_dims& d = P->d;
+    const int T = P->T, E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, B = d.batch, S = d.seq;
+    const int L2E = P->L2E;
+    const ergm_model_params& p = P->p;
+
+    if (!P->dry)
+        ERGM_TRY(ergm_embed_fwd(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap, B,
+                            S, E, d.vocab, s));
+    // all L cross-attention K/V projections of the caption embeddings in one GEMM
+    ERGM_TRY(gemm(P, s, T, L2E, E, P->cap, E, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
+                  ERGM_EPI_BIAS, p.capkv_b));
+    for (int l = 0; l < L; ++l) {
+        LayerActs& a = P->la[l];
+        float* x0 = P->resid[3 * l];
+        float* x1 = P->resid[3 * l + 1];
+        float* x2 = P->resid[3 * l + 2];
+        float* x3 = P->resid[3 * l + 3];
+        // self-attention sub-block (src/model.py:297-309)
+        if (!P->dry)
+            ERGM_TRY(ergm_layernorm_fwd(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, a.m1, a.r1, T, E, d.eps, s));
+        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
+                      ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+        if (!P->dry)
+            ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, B, H, S, S, 3 * E, 3 * E, 3 * E, E, 1, s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.ao, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+        // cross-attention over caption embeddings (src/model.py:311-329)
+        if (!P->dry)
+            ERGM_TRY(ergm_layernorm_fwd(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, a.mx, a.rx, T, E, d.eps, s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
+                      ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+        const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
+        if (!P->dry)
+            ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, E, 0, s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.xo, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+        // MLP (src/model.py:331-334, 262-267)
+        if (!P->dry)
+            ERGM_TRY(ergm_layernorm_fwd(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, a.m2, a.r2, T, E, d.eps, s));
+        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, E, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, F, ERGM_BF16,
+                      ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+        ERGM_TRY(gemm(P, s, T, E, F, a.act, F, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+    }
+    if (!P->dry)
+        ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));
+    // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
+    ERGM_TRY(gemm(P, s, T, d.vocab_pad, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad, ERGM_BF16,
+                  ERGM_EPI_NONE));
+    if (P->dry) return ERGM_OK;
+    ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, B, S, E, 7,
+                               P->B_global, nullptr, s));
+    if (P->labels) {
+        ERGM_TRY(ergm_xent_fwd_bwd(logits, d.vocab_pad, P->labels, P->n_valid, P->row_loss, train ? P->dlogits : nullptr,
+                                   B, S, d.vocab, 1.0f, s));
+    } else if (train) {
+        ERGM_TRY(hipMemsetAsync(P->dlogits, 0, (size_t)T * d.vocab_pad * 2, s) == hipSuccess ? ERGM_OK : ERGM_EHIP);
+        ERGM_TRY(hipMemsetAsync(P->row_loss, 0, (size_t)T * 4, s) == hipSuccess ? ERGM_OK : ERGM_EHIP);
+    }
+    if (P->labels || P->emo_labels) {
+        if (!P->labels) ERGM_TRY(hipMemsetAsync(P->row_loss, 0, (size_t)T * 4, s) == hipSuccess ? ERGM_OK : ERGM_EHIP);
+        ERGM_TRY(ergm_loss_finalize(P->row_loss, T, P->labels ? P->n_valid : nullptr,
+                                    P->emo_labels ? P->emo_sum : nullptr, P->B_global, out_loss, s));
+    }
+    P->have_fwd = train != 0;
+    return check_launch("model_forward");
+}
+
+}  // namespace
+
+extern "C" int ergm_model_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train,
+                                  void* stream) {
+    ERGM_CHECK_ARG(P && logits && emo_logits, "model_forward: null argument");
+    ERGM_CHECK_ARG(P->ids, "model_forward: call ergm_model_set_inputs first");
+    ERGM_CHECK_ARG(!(P->labels || P->emo_labels) || out_loss, "model_forward: labels need out_loss");
+    return do_forward(P, logits, emo_logits, out_loss, train, as_stream(stream));
+}
+
+namespace {
+
+int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
+    const ergm_model_dims& d = P->d;
+    const ergm_model_params& p = P->p;
+    const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad;
+    // dh_f = dlogits · wte  (contraction over the padded vocab), dwte = dlogitsᵀ · ln_f(h)
+    ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
+                  nullptr, nullptr, 0, nullptr, 0, gscale));
+    ERGM_TRY(gemm(P, s, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32, ERGM_EPI_NONE,
+                  nullptr, nullptr, 0, nullptr, 0, gscale));
+    if (P->dry) return ERGM_OK;
+    if (P->emo_labels) {
+        ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w, P->dy, B,
+                                   S, E, 7, P->B_global, gscale, s));
+    } else {
+        if (hipMemsetAsync(p.g_emo_w, 0, (size_t)7 * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
+    }
+    if (hipMemsetAsync(P->dh, 0, (size_t)T * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
+    return ln_bwd(P, s, P->resid[3 * d.n_layer], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b);
+}
+
+int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
+    const ergm_model_dims& d = P->d;
+    const int T = P->T, E = d.n_embd, F = d.n_inner, H = d.n_head, B = d.batch, S = d.seq, L2E = P->L2E;
+    LayerActs a = P->dry ? LayerActs{} : P->la[l];
+    const float* x0 = P->dry ? nullptr : P->resid[3 * l];
+    const float* x1 = P->dry ? nullptr : P->resid[3 * l + 1];
+    const float* x2 = P->dry ? nullptr : P->resid[3 * l + 2];
+    // ---- MLP: x3 = x2 + gelu(ln2(x2)·Wfc + bfc)·Wm + bm
+    ERGM_TRY(gemm(P, s, F, E, T, a.act, F, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_MPROJ_W), E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_MPROJ_B)));
+    ERGM_TRY(gemm(P, s, T, F, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK, P->dpre, F, ERGM_BF16,
+                  ERGM_EPI_GELU_BWD, nullptr, a.pre, F));
+    ERGM_TRY(gemm(P, s, E, F, T, a.ln2, E, ERGM_KM, P->dpre, F, ERGM_KN, LG(P, l, ERGM_T_FC_W), F, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dpre, ERGM_BF16, T, F, F, LG(P, l, ERGM_T_FC_B)));
+    ERGM_TRY(gemm(P, s, T, E, F, P->dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
+    // ---- cross-attention: x2 = x1 + Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp
+    ERGM_TRY(gemm(P, s, E, E, T, a.xo, E, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_XPROJ_W), E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_XPROJ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
+                  ERGM_EPI_NONE));
+    if (!P->dry) {
+        const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
+        __bf16* dkl = P->dkv_all + (size_t)l * 2 * E;
+        ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, P->dxq, dkl, dkl + E, B, H, S, S, E,
+                               L2E, L2E, E, E, E, L2E, L2E, 0, s));
+    }
+    ERGM_TRY(gemm(P, s, E, E, T, a.lnx, E, ERGM_KM, P->dxq, E, ERGM_KN, LG(P, l, ERGM_T_XQ_W), E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dxq, ERGM_BF16, T, E, E, LG(P, l, ERGM_T_XQ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, P->dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
+    // ---- self-attention: x1 = x0 + Attn(ln_1(x0)·Wqkv + b)·Wap + bap
+    ERGM_TRY(gemm(P, s, E, E, T, a.ao, E, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_APROJ_W), E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_APROJ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
+                  ERGM_EPI_NONE));
+    if (!P->dry) {
+        ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, P->dqkv, P->dqkv + E,
+                               P->dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, E, E, 3 * E, 3 * E, 3 * E, 1, s));
+    }
+    ERGM_TRY(gemm(P, s, E, 3 * E, T, a.ln1, E, ERGM_KM, P->dqkv, 3 * E, ERGM_KN, LG(P, l, ERGM_T_ATTN_W), 3 * E,
+                  ERGM_F32, ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dqkv, ERGM_BF16, T, 3 * E, 3 * E, LG(P, l, ERGM_T_ATTN_B)));
+    ERGM_TRY(gemm(P, s, T, E, 3 * E, P->dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
+                  ERGM_F32, ERGM_EPI_NONE));
+    return ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B));
+}
+
+int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
+    const ergm_model_dims& d = P->d;
+    const ergm_model_params& p = P->p;
+    const int T = P->T, E = d.n_embd, L2E = P->L2E;
+    // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all, dcap = dKV_all·Wᵀ
+    ERGM_TRY(gemm(P, s, E, L2E, T, P->cap, E, ERGM_KM, P->dkv_all, L2E, ERGM_KN, p.g_capkv_w, L2E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    ERGM_TRY(colsum(P, s, P->dkv_all, ERGM_BF16, T, L2E, L2E, p.g_capkv_b));
+    ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
+                  ERGM_EPI_NONE));
+    if (P->dry) return ERGM_OK;
+    return ergm_embed_bwd(P->ids, P->tt, P->cap_ids, P->dh, P->dcap, p.g_wte, p.g_wpe, P->scratch, P->scratch_bytes,
+                          d.batch, d.seq, E, d.vocab, s);
+}
+
+}  // namespace
+
+extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale, void* stream) {
+    ERGM_CHECK_ARG(P, "model_backward_head: null plan");
+    ERGM_CHECK_ARG(P->have_fwd, "model_backward_head: no training forward to differentiate");
+    return do_backward_head(P, gscale, as_stream(stream));
+}
+
+extern "C" int ergm_model_backward_layer(ergm_model_plan* P, int layer, void* stream) {
+    ERGM_CHECK_ARG(P && layer >= 0 && layer < P->d.n_layer, "model_backward_layer: bad layer");
+    ERGM_CHECK_ARG(P->have_fwd, "model_backward_layer: no training forward to differentiate");
+    return do_backward_layer(P, layer, as_stream(stream));
+}
+
+extern "C" int ergm_model_backward_embed(ergm_model_plan* P, void* stream) {
+    ERGM_CHECK_ARG(P, "model_backward_embed: null plan");
+    ERGM_CHECK_ARG(P->have_fwd, "model_backward_embed: no training forward to differentiate");
+    return do_backward_embed(P, as_stream(stream));
+}

@@ -1,0 +1,285 @@
+// LayerNorm forward/backward and deterministic column sums for gfx950.
+//
+// Replaces nn.LayerNorm (ln_1 / ln_cross_attn / ln_2 / ln_f: src/model.py:276,278,282,392, applied at
+// :298,318,332,578) and its autograd backward; column sums give Conv1D bias gradients, the LayerNorm
+// dγ/dβ reductions and the wpe gradient (Σ over batch of the embedding gradient).
+// Row-per-wavefront: each lane owns NV float4 column groups of the row (coalesced 1 KiB per
+// wave-instruction), reductions by 64-lane xor shuffles; HBM-bound.
+#include "common.h"
+
+namespace ergm {
+
+constexpr int LN_ROWS_PER_BLOCK_BWD = 32;
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, __bf16* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int E, float eps) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;
+    const float* xr = x + (size_t)row * E;
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int c = (i * 64 + lane) * 4;
+        v[i] = c < E ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0, 0, 0, 0);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float inv_e = 1.0f / (float)E;
+    const float mean = wave_sum(s) * inv_e;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int c = (i * 64 + lane) * 4;
+        if (c < E) {
+            float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+            q += (a * a + b * b) + (cc * cc + d * d);
+        }
+    }
+    const float var = wave_sum(q) * inv_e;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int c = (i * 64 + lane) * 4;
+        if (c < E) {
+            float4 g = *reinterpret_cast<const float4*>(gamma + c);
+            float4 b = *reinterpret_cast<const float4*>(beta + c);
+            bf16x4 o;
+            o[0] = f2bf((v[i].x - mean) * rstd * g.x + b.x);
+            o[1] = f2bf((v[i].y - mean) * rstd * g.y + b.y);
+            o[2] = f2bf((v[i].z - mean) * rstd * g.z + b.z);
+            o[3] = f2bf((v[i].w - mean) * rstd * g.w + b.w);
+            *reinterpret_cast<bf16x4*>(y + (size_t)row * E + c) = o;
+        }
+    }
+    if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+}
+
+// dx = rstd·(g − mean(g) − x̂·mean(g·x̂)), g = dy·γ;  dres += dx;  partial dγ = Σ dy·x̂, dβ = Σ dy
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const float* __restrict__ gamma, float* __restrict__ dres,
+                                                     __bf16* __restrict__ dres_b, float* __restrict__ part_g,
+                                                     float* __restrict__ part_b, int rows, int E) {
+    __shared__ float red[2][4][NV * 256];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float4 pg[NV], pb[NV], gm[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        pg[i] = make_float4(0, 0, 0, 0);
+        pb[i] = make_float4(0, 0, 0, 0);
+        int c = (i * 64 + lane) * 4;
+        gm[i] = c < E ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0, 0, 0, 0);
+    }
+    const float inv_e = 1.0f / (float)E;
+    const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD;
+    for (int rr = wave; rr < LN_ROWS_PER_BLOCK_BWD; rr += 4) {
+        const int row = r0 + rr;
+        if (row >= rows) break;
+        const float mu = mean_in[row], rs = rstd_in[row];
+        float4 xh[NV], g[NV], d[NV];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            int c = (i * 64 + lane) * 4;
+            if (c < E) {
+                float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * E + c);
+                d[i] = *reinterpret_cast<const float4*>(dy + (size_t)row * E + c);
+                xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+            } else {
+                d[i] = make_float4(0, 0, 0, 0);
+                xh[i] = make_float4(0, 0, 0, 0);
+            }
+            g[i] = make_float4(d[i].x * gm[i].x, d[i].y * gm[i].y, d[i].z * gm[i].z, d[i].w * gm[i].w);
+            s1 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+            s2 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
+            pg[i].x += d[i].x * xh[i].x; pg[i].y += d[i].y * xh[i].y;
+            pg[i].z += d[i].z * xh[i].z; pg[i].w += d[i].w * xh[i].w;
+            pb[i].x += d[i].x; pb[i].y += d[i].y; pb[i].z += d[i].z; pb[i].w += d[i].w;
+        }
+        const float c1 = wave_sum(s1) * inv_e, c2 = wave_sum(s2) * inv_e;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            int c = (i * 64 + lane) * 4;
+            if (c < E) {
+                float* dp = dres + (size_t)row * E + c;
+                float4 o = *reinterpret_cast<float4*>(dp);
+                o.x += rs * (g[i].x - c2 - xh[i].x * c1);
+                o.y += rs * (g[i].y - c2 - xh[i].y * c1);
+                o.z += rs * (g[i].z - c2 - xh[i].z * c1);
+                o.w += rs * (g[i].w - c2 - xh[i].w * c1);
+                *reinterpret_cast<float4*>(dp) = o;
+                if (dres_b) {
+                    bf16x4 ob;
+                    ob[0] = f2bf(o.x); ob[1] = f2bf(o.y); ob[2] = f2bf(o.z); ob[3] = f2bf(o.w);
+                    *reinterpret_cast<bf16x4*>(dres_b + (size_t)row * E + c) = ob;
+                }
+            }
+        }
+    }
+    // cross-wave reduction of the partial column sums (fixed order → deterministic)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int c = (i * 64 + lane) * 4;
+        *reinterpret_cast<float4*>(&red[0][wave][c]) = pg[i];
+        *reinterpret_cast<float4*>(&red[1][wave][c]) = pb[i];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < E; c += 256) {
+        float a = ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
+        float b = ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+        part_g[(size_t)blockIdx.x * E + c] = a;
+        part_b[(size_t)blockIdx.x * E + c] = b;
+    }
+}
+
+// ---- column sums: out[c] (+)= Σ_r X[r][c] -------------------------------------------------
+constexpr int CS_ROWS = 64;  // rows per partial block
+
+template <bool BF16_IN>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restrict__ X, int rows, int cols, int ldx,
+                                                             float* __restrict__ part, float* __restrict__ out,
+                                                             int accumulate, int direct) {
+    // block: 64 column groups (4 cols each) x 4 row lanes; blockIdx.x: 256-column slab, y: row chunk
+    __shared__ float4 red[4][64];
+    const int cg = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    const int c = (blockIdx.x * 64 + cg) * 4;
+    const int r0 = blockIdx.y * CS_ROWS;
+    float4 s = make_float4(0, 0, 0, 0);
+    if (c < cols) {
+        for (int r = r0 + rl; r < min(rows, r0 + CS_ROWS); r += 4) {
+            float4 v;
+            if (BF16_IN) {
+                bf16x4 b = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(X) + (size_t)r * ldx + c);
+                v = make_float4(bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3]));
+            } else {
+                v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + (size_t)r * ldx + c);
+            }
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    }
+    red[rl][cg] = s;
+    __syncthreads();
+    if (rl == 0 && c < cols) {
+        float4 t = red[0][cg];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            t.x += red[k][cg].x; t.y += red[k][cg].y; t.z += red[k][cg].z; t.w += red[k][cg].w;
+        }
+        if (direct) {
+            float4* o = reinterpret_cast<float4*>(out + c);
+            if (accumulate) {
+                float4 p = *o;
+                t.x += p.x; t.y += p.y; t.z += p.z; t.w += p.w;
+            }
+            *o = t;
+        } else {
+            *reinterpret_cast<float4*>(part + (size_t)blockIdx.y * cols + c) = t;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nparts, int cols,
+                                                           float* __restrict__ out, int accumulate) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int p = 0; p < nparts; ++p) s += part[(size_t)p * cols + c];
+    if (accumulate) s += out[c];
+    out[c] = s;
+}
+
+int colsum_impl(const void* X, bool bf16_in, int rows, int cols, int ldx, float* out, int accumulate, float* ws,
+                size_t ws_bytes, hipStream_t s) {
+    int nparts = cdiv(rows, CS_ROWS);
+    dim3 grid(cdiv(cols, 256), nparts);
+    bool direct = nparts == 1;
+    if (!direct) {
+        size_t need = (size_t)nparts * cols * sizeof(float);
+        ERGM_CHECK_ARG(ws && ws_bytes >= need, "colsum: workspace %zu < %zu", ws_bytes, need);
+    }
+    if (bf16_in)
+        hipLaunchKernelGGL(colsum_partial_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
+                           (int)direct);
+    else
+        hipLaunchKernelGGL(colsum_partial_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
+                           (int)direct);
+    if (!direct)
+        hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, s, ws, nparts, cols, out,
+                           accumulate);
+    return check_launch("colsum");
+}
+
+size_t colsum_ws(int rows, int cols) {
+    int nparts = cdiv(rows, CS_ROWS);
+    return nparts > 1 ? (size_t)nparts * cols * sizeof(float) : 0;
+}
+
+}  // namespace ergm
+
+using namespace ergm;
+
+extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
+                                  float* rstd, int rows, int E, float eps, void* stream) {
+    ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
+    ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_fwd: unsupported E=%d", E);
+    dim3 grid(cdiv(rows, 4));
+    hipStream_t s = as_stream(stream);
+    int nv = cdiv(E, 256);
+    auto* yb = reinterpret_cast<__bf16*>(y);
+    switch (nv) {
+        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
+        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
+        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
+        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
+    }
+    return check_launch("layernorm_fwd");
+}
+
+extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {
+    int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
+    return 2 * (size_t)nb * E * sizeof(float) + colsum_ws(nb, E);
+}
+
+extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                                  const float* gamma, float* dres, void* dres_bf16, float* dgamma, float* dbeta,
+                                  void* ws, size_t ws_bytes, int rows, int E, void* stream) {
+    ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && dgamma && dbeta, "layernorm_bwd: null argument");
+    ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
+    ERGM_CHECK_ARG(ws && ws_bytes >= ergm_layernorm_bwd_workspace_size(rows, E), "layernorm_bwd: workspace too small");
+    int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
+    float* pg = reinterpret_cast<float*>(ws);
+    float* pb = pg + (size_t)nb * E;
+    float* cws = pb + (size_t)nb * E;
+    size_t cws_bytes = ws_bytes - 2 * (size_t)nb * E * sizeof(float);
+    hipStream_t s = as_stream(stream);
+    auto* db = reinterpret_cast<__bf16*>(dres_bf16);
+    int nv = cdiv(E, 256);
+    switch (nv) {
+        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
+        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
+        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
+        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
+    }
+    ERGM_TRY(check_launch("layernorm_bwd"));
+    ERGM_TRY(colsum_impl(pg, false, nb, E, E, dgamma, 0, cws, cws_bytes, s));
+    return colsum_impl(pb, false, nb, E, E, dbeta, 0, cws, cws_bytes, s);
+}
+
+extern "C" size_t ergm_colsum_workspace_size(int rows, int cols) { return colsum_ws(rows, cols); }
+
+extern "C" int ergm_colsum(const void* X, int x_dtype, int rows, int cols, int ldx, float* out, int accumulate,
+                           void* ws, size_t ws_bytes, void* stream) {
+    ERGM_CHECK_ARG(X && out, "colsum: null argument");
+    ERGM_CHECK_ARG(rows > 0 && cols > 0 && cols % 4 == 0 && ldx % 4 == 0 && ldx >= cols, "colsum: bad shape");
+    ERGM_CHECK_ARG(x_dtype == ERGM_F32 || x_dtype == ERGM_BF16, "colsum: bad dtype");
+    return colsum_impl(X, x_dtype == ERGM_BF16, rows, cols, ldx, out, accumulate, reinterpret_cast<float*>(ws),
+                       ws_bytes, as_stream(stream));
+}

@@ -1,0 +1,186 @@
+"""Tensor-level wrappers over the C-ABI kernels (one HIP launch sequence per call).
+
+Every function takes torch tensors that already live on the GPU, checks shapes/dtypes on the host,
+and calls the corresponding ``ergm_*`` entry point on the current HIP stream.  No function falls back
+to PyTorch or CPU: a missing library or a non-GPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(dev: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("ergm_amd ops need GPU tensors (the HIP path has no CPU fallback)")
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int = L.MK, b_layout: int = L.NK,
+         out: Optional[torch.Tensor] = None, out_dtype=torch.float32, epilogue: int = L.EPI_NONE,
+         bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+         aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0, split_k: int = 0,
+         alpha_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C[M,N] = epilogue(alpha · A·B); A/B bf16 row-major with layouts as in ergm_hip.h."""
+    _need_gpu(A, B)
+    assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
+    lda = A.stride(0) if A.dim() == 2 else (K if a_layout == L.MK else M)
+    ldb = B.stride(0) if B.dim() == 2 else (K if b_layout == L.NK else N)
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=A.device)
+    d = L.GemmDesc(M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=out.stride(0), a_layout=a_layout, b_layout=b_layout,
+                   c_dtype=L.BF16 if out.dtype == torch.bfloat16 else L.F32, epilogue=epilogue, alpha=alpha,
+                   bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
+                   aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0,
+                   split_k=split_k, alpha_dev=_ptr(alpha_dev))
+    lib = L.load()
+    wsb = lib.ergm_gemm_workspace_size(C.byref(d))
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=A.device)
+    L.check(lib.ergm_gemm(C.byref(d), _ptr(A), _ptr(B), _ptr(out), _ptr(ws), wsb, _stream(A.device)), "ergm_gemm")
+    return out
+
+
+def attn_fwd(q, k, v, B, H, Sq, Sk, causal, o=None, lse=None):
+    """q/k/v: 2-D token-major views [B*S, ld] whose first column is head 0, dim 0."""
+    _need_gpu(q, k, v)
+    dev = q.device
+    if o is None:
+        o = torch.empty(B * Sq, H * 64, dtype=torch.bfloat16, device=dev)
+    if lse is None:
+        lse = torch.empty(B, H, Sq, dtype=torch.float32, device=dev)
+    L.call("ergm_attn_fwd", _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, q.stride(0), k.stride(0),
+           v.stride(0), o.stride(0), int(bool(causal)), _stream(dev))
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal, dq=None, dk=None, dv=None):
+    _need_gpu(q, k, v, o, dout, lse)
+    dev = q.device
+    dq = torch.empty(B * Sq, H * 64, dtype=torch.bfloat16, device=dev) if dq is None else dq
+    dk = torch.empty(B * Sk, H * 64, dtype=torch.bfloat16, device=dev) if dk is None else dk
+    dv = torch.empty(B * Sk, H * 64, dtype=torch.bfloat16, device=dev) if dv is None else dv
+    delta = torch.empty(B, H, Sq, dtype=torch.float32, device=dev)
+    L.call("ergm_attn_bwd", _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
+           _ptr(dv), B, H, Sq, Sk, q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0), dq.stride(0),
+           dk.stride(0), dv.stride(0), int(bool(causal)), _stream(dev))
+    return dq, dk, dv
+
+
+def layernorm_fwd(x, gamma, beta, eps=1e-5):
+    _need_gpu(x, gamma, beta)
+    rows, E = x.shape
+    y = torch.empty(rows, E, dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    L.call("ergm_layernorm_fwd", _ptr(x), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), rows, E, eps,
+           _stream(x.device))
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dres):
+    """dres += LN_bwd(dy) in place; returns (dres, dres_bf16, dgamma, dbeta)."""
+    _need_gpu(dy, x, mean, rstd, gamma, dres)
+    rows, E = x.shape
+    lib = L.load()
+    wsb = lib.ergm_layernorm_bwd_workspace_size(rows, E)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x.device)
+    db = torch.empty(rows, E, dtype=torch.bfloat16, device=x.device)
+    dg = torch.empty(E, dtype=torch.float32, device=x.device)
+    dbe = torch.empty_like(dg)
+    L.call("ergm_layernorm_bwd", _ptr(dy), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dres), _ptr(db), _ptr(dg),
+           _ptr(dbe), _ptr(ws), wsb, rows, E, _stream(x.device))
+    return dres, db, dg, dbe
+
+
+def colsum(X, out=None, accumulate=False):
+    _need_gpu(X)
+    rows, cols = X.shape
+    out = torch.zeros(cols, dtype=torch.float32, device=X.device) if out is None else out
+    lib = L.load()
+    wsb = lib.ergm_colsum_workspace_size(rows, cols)
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=X.device)
+    L.call("ergm_colsum", _ptr(X), L.BF16 if X.dtype == torch.bfloat16 else L.F32, rows, cols, X.stride(0), _ptr(out),
+           int(accumulate), _ptr(ws), wsb, _stream(X.device))
+    return out
+
+
+def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None):
+    _need_gpu(ids, cap_ids, wte, wpe)
+    B, S = ids.shape
+    V, E = wte.shape
+    h0 = torch.empty(B * S, E, dtype=torch.float32, device=ids.device)
+    cap = torch.empty(B * S, E, dtype=torch.bfloat16, device=ids.device)
+    ld_vis = 0
+    if vis is not None:
+        vis = vis.contiguous()
+        ld_vis = vis[0].numel() if vis.dim() == 3 else vis.shape[1]
+    L.call("ergm_embed_fwd", _ptr(ids), _ptr(tt), _ptr(cap_ids), _ptr(wte), _ptr(wpe), _ptr(vis), ld_vis,
+           _ptr(aud), _ptr(h0), _ptr(cap), B, S, E, V, _stream(ids.device))
+    return h0, cap
+
+
+def embed_bwd(ids, tt, cap_ids, dh0, dcap, dwte, dwpe):
+    B, S = ids.shape
+    V, E = dwte.shape
+    lib = L.load()
+    wsb = lib.ergm_embed_bwd_workspace_size(B * S)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=ids.device)
+    L.call("ergm_embed_bwd", _ptr(ids), _ptr(tt), _ptr(cap_ids), _ptr(dh0), _ptr(dcap), _ptr(dwte), _ptr(dwpe),
+           _ptr(ws), wsb, B, S, E, V, _stream(ids.device))
+
+
+def count_valid(labels):
+    B, S = labels.shape
+    out = torch.empty(1, dtype=torch.int32, device=labels.device)
+    L.call("ergm_count_valid", _ptr(labels), B, S, _ptr(out), _stream(labels.device))
+    return out
+
+
+def xent(logits, labels, n_valid, V, with_grad=True):
+    """logits: [B*S, ldl] bf16.  Returns (row_loss[B*S], dlogits or None)."""
+    B, S = labels.shape
+    rl = torch.empty(B * S, dtype=torch.float32, device=logits.device)
+    dl = torch.empty_like(logits) if with_grad else None
+    L.call("ergm_xent_fwd_bwd", _ptr(logits), logits.stride(0), _ptr(labels), _ptr(n_valid), _ptr(rl), _ptr(dl), B, S, V,
+           1.0, _stream(logits.device))
+    return rl, dl
+
+
+def emotion_head(h, W, labels, B, S, B_global=None, dh=None, grad_scale=None):
+    E = h.shape[-1]
+    Cn = W.shape[0]
+    logits = torch.empty(B, Cn, dtype=torch.float32, device=h.device)
+    loss_sum = torch.empty(1, dtype=torch.float32, device=h.device)
+    dW = torch.empty_like(W) if dh is not None else None
+    L.call("ergm_emotion_head", _ptr(h), _ptr(W), _ptr(labels), _ptr(logits), _ptr(loss_sum), _ptr(dW), _ptr(dh), B, S,
+           E, Cn, B_global or B, _ptr(grad_scale), _stream(h.device))
+    return logits, loss_sum, dW
+
+
+def adamw_step(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step):
+    """One torch.optim.AdamW step (flat fp32 buffers), bias corrections formed in double like torch."""
+    import math
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    L.call("ergm_adamw_step", _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
+           weight_decay, lr / bc1, math.sqrt(bc2), _stream(p.device))
+
+
+def cast_bf16(src, dst):
+    L.call("ergm_cast_bf16", _ptr(src), _ptr(dst), src.numel(), _stream(src.device))
+
+
+def axpy(x, y, alpha=1.0):
+    L.call("ergm_axpy", _ptr(x), _ptr(y), x.numel(), alpha, _stream(x.device))

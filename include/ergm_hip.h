@@ -1,0 +1,242 @@
+/*
+ * ergm_hip.h — C-ABI of libergm_hip.so, the MI355X (gfx950) implementation of ERGM's fused GPT-2
+ * training step (LovesickPatience/ERGM src/model.py + the src/main.py train step).
+ *
+ * Every entry point is `extern "C"`, takes plain pointers + sizes + an explicit hipStream_t
+ * (passed as void*), never allocates on the hot path (the caller passes workspace), never frees or
+ * retains caller memory, and returns 0 (ERGM_OK) or a negative ergm_status.  A thread-local
+ * message is kept for the last error (ergm_last_error).  All calls are asynchronous on `stream`,
+ * re-entrant and callable from any host thread (PyTorch's autograd worker thread included).
+ *
+ * Which reference interface each entry replaces (paths relative to /root/reference):
+ *   ergm_gemm             transformers Conv1D.forward (addmm, W stored [in,out]) used at
+ *                         src/model.py:95-99,257-258 and its autograd backward (dX = dY·Wᵀ,
+ *                         dW = Xᵀ·dY); nn.Linear lm_head (src/model.py:605,698)
+ *   ergm_attn_fwd         GPT2Attention._attn src/model.py:119-148 (+ _split_heads/_merge_heads
+ *                         :190-198 folded into addressing)
+ *   ergm_attn_bwd         autograd backward of the same
+ *   ergm_layernorm_fwd    nn.LayerNorm (src/model.py:276,278,282,392; applied :298,318,332,578)
+ *   ergm_layernorm_bwd    its autograd backward
+ *   ergm_embed_fwd        wte/wpe lookups + visual/audio injection + token-type add
+ *                         (src/model.py:459-463,495-504)
+ *   ergm_embed_bwd        Embedding backward into the tied wte / wpe
+ *   ergm_xent_fwd_bwd     CrossEntropyLoss(ignore_index=-100) on shifted logits (src/model.py:704-708)
+ *   ergm_emotion_head     emotion_head + its CrossEntropyLoss (src/model.py:700-701,710-711)
+ *   ergm_adamw_step       torch.optim.AdamW.step (src/main.py:68,155)
+ *   ergm_model_*          the whole GPT2LMHeadModel.forward (src/model.py:654-737) and its
+ *                         backward (src/main.py:154) as one native launch sequence
+ */
+#ifndef ERGM_HIP_H
+#define ERGM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ERGM_ABI_VERSION 1
+
+typedef enum {
+    ERGM_OK = 0,
+    ERGM_EINVAL = -1,        /* bad shape / stride / dtype / alignment / null pointer */
+    ERGM_EUNSUPPORTED = -2,  /* valid request this build does not implement */
+    ERGM_EHIP = -3,          /* HIP launch / runtime failure (hipError_t in the message) */
+} ergm_status;
+
+typedef enum { ERGM_F32 = 0, ERGM_BF16 = 1 } ergm_dtype;
+
+/* Operand storage layouts (row-major storage, leading dimension in elements).
+ *   A: ERGM_MK = A[m][k] (k contiguous)   ERGM_KM = A[k][m] (m contiguous)
+ *   B: ERGM_NK = B[n][k] (nn.Linear weight, k contiguous)
+ *      ERGM_KN = B[k][n] (Conv1D weight [in,out], n contiguous)                    */
+typedef enum { ERGM_MK = 0, ERGM_KM = 1 } ergm_a_layout;
+typedef enum { ERGM_NK = 0, ERGM_KN = 1 } ergm_b_layout;
+
+/* Epilogues applied to v = alpha * (A·B)[m][n] (all math fp32):
+ *   NONE        C = v
+ *   BIAS        C = v + bias[n]
+ *   BIAS_GELU   aux_out[m][n] = bf16(v + bias[n]) (pre-activation, for backward);
+ *               C = gelu_new(v + bias[n])
+ *   BIAS_RESID  C(f32) = aux[m][n](f32) + (v + bias[n])          (residual add; aux may == C)
+ *   GELU_BWD    C = v * gelu_new'(aux[m][n]) with aux = bf16 pre-activation
+ *   ACCUM       C(f32) = C + v                                   (beta = 1 accumulation)          */
+typedef enum {
+    ERGM_EPI_NONE = 0,
+    ERGM_EPI_BIAS = 1,
+    ERGM_EPI_BIAS_GELU = 2,
+    ERGM_EPI_BIAS_RESID = 3,
+    ERGM_EPI_GELU_BWD = 4,
+    ERGM_EPI_ACCUM = 5,
+} ergm_epilogue;
+
+typedef struct {
+    int M, N, K;
+    int lda, ldb, ldc;
+    int a_layout;   /* ergm_a_layout */
+    int b_layout;   /* ergm_b_layout */
+    int c_dtype;    /* ergm_dtype of C (A and B are bf16) */
+    int epilogue;   /* ergm_epilogue */
+    float alpha;
+    const float* bias;   /* [N] f32 or NULL */
+    const void* aux;     /* epilogue input: f32 residual [M][ld_aux] or bf16 pre-activation */
+    int ld_aux;
+    void* aux_out;       /* epilogue second output (bf16 pre-activation) [M][ld_aux_out] */
+    int ld_aux_out;
+    int split_k;         /* 0 = choose automatically, 1 = none, >1 = forced split count */
+    const float* alpha_dev;  /* optional device scalar multiplied into alpha (autograd grad_output) */
+} ergm_gemm_desc;
+
+/* Workspace bytes ergm_gemm needs for `desc` (split-K partial slabs); 0 if none. */
+size_t ergm_gemm_workspace_size(const ergm_gemm_desc* desc);
+int ergm_gemm(const ergm_gemm_desc* desc, const void* A, const void* B, void* C, void* workspace,
+              size_t ws_bytes, void* stream);
+
+/* Fused attention over head_dim = 64, token-major tensors with head h at columns [64h, 64h+64):
+ *   Q[b][s][h*64+d] = q + (b*Sq + s)*ldq + h*64 + d     (likewise K/V with Sk rows, O with ldo)
+ * out: O (bf16) and lse[b][h][s] = ln Σ_k exp(score) (f32; backward recomputes P from it).
+ * `causal`: key j visible to query i iff j <= i (Sq == Sk required). scale = 1/sqrt(64).          */
+int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
+                  int Sq, int Sk, int ldq, int ldk, int ldv, int ldo, int causal, void* stream);
+/* delta workspace: B*H*Sq floats.  dq/dk/dv are bf16 with their own leading dims.              */
+int ergm_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                  const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
+                  int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
+                  int causal, void* stream);
+
+/* LayerNorm over rows of E (biased variance, eps): y(bf16) = (x-μ)·rstd·γ + β; x f32.        */
+int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
+                       float* rstd, int rows, int E, float eps, void* stream);
+/* dres(f32, in/out) += LN_bwd(dy); dres_bf16 (optional) = bf16(dres); dγ/dβ (f32 [E], written).
+ * workspace: ergm_layernorm_bwd_workspace_size(rows, E) bytes.                                  */
+size_t ergm_layernorm_bwd_workspace_size(int rows, int E);
+int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, float* dres, void* dres_bf16, float* dgamma, float* dbeta,
+                       void* workspace, size_t ws_bytes, int rows, int E, void* stream);
+
+/* Column sums of a row-major matrix (bias gradients, wpe gradient): out[c] (=|+=) Σ_r X[r][c]. */
+size_t ergm_colsum_workspace_size(int rows, int cols);
+int ergm_colsum(const void* X, int x_dtype, int rows, int cols, int ldx, float* out, int accumulate,
+                void* workspace, size_t ws_bytes, void* stream);
+
+/* Embedding + fusion (src/model.py:459-463,495-504):
+ *   h0[b,s] = ((wte[ids] + [s==0]·vis[b] + [s==1]·aud[b]) + wpe[s]) + wte[tt]      (f32)
+ *   cap[b,s] = bf16(wte[cap_ids])
+ * vis: [B][ld_vis] row b's first E values (imgs[i][0]); vis/aud may be NULL (text-only);
+ * tt may be NULL.                                                                              */
+int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
+                   const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0,
+                   void* cap, int B, int S, int E, int V, void* stream);
+/* Deterministic (sorted segment-sum) embedding backward:
+ *   dwte[v] += Σ_{t: ids[t]=v} dh0[t] + Σ_{t: tt[t]=v} dh0[t] + Σ_{t: cap[t]=v} dcap[t]
+ *   dwpe[s]  = Σ_b dh0[b,s]
+ * workspace: ergm_embed_bwd_workspace_size(B*S) bytes.                                          */
+size_t ergm_embed_bwd_workspace_size(int T);
+int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* dh0,
+                   const float* dcap, float* dwte, float* dwpe, void* workspace, size_t ws_bytes,
+                   int B, int S, int E, int V, void* stream);
+
+/* Shifted LM cross-entropy, fused forward+backward over bf16 logits [B*S][ldl] (columns >= V
+ * ignored, zeroed in dlogits).  Row t=(b,s) is valid iff s < S-1 and labels[b][s+1] != -100.
+ * n_valid_global: device int (count of valid rows over all DP ranks).
+ * row_loss[t] = lse - logit[target] (0 for invalid); dlogits = grad_scale·(softmax - onehot)/n_valid
+ * (bf16, may be NULL for forward only).  ergm_count_valid writes the local count.             */
+int ergm_count_valid(const int64_t* labels, int B, int S, int* n_valid, void* stream);
+int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* labels, const int* n_valid_global,
+                      float* row_loss, void* dlogits, int B, int S, int V, float grad_scale,
+                      void* stream);
+/* Emotion head on the last token: logits[b][c] = Σ_e h[b,S-1,e]·W[c][e] (h bf16, W f32 [C][E]);
+ * if labels: loss_out = mean CE over B_global (loss_sum written), dW[C][E] written,
+ * dh[b,S-1,:] += dlogits·W (f32 dh [B*S][E]).                                                   */
+int ergm_emotion_head(const void* h, const float* W, const int64_t* labels, float* logits,
+                      float* loss_sum, float* dW, float* dh, int B, int S, int E, int C,
+                      int B_global, const float* grad_scale_dev, void* stream);
+/* out[0] = Σ row_loss / n_valid_global (0 if n_valid_global is NULL), out[1] = emo_loss_sum / B_global, out[2] = out[0]+out[1]. */
+int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
+                       const float* emo_loss_sum, int B_global, float* out, void* stream);
+
+/* torch.optim.AdamW step over flat fp32 arrays; also refreshes the bf16 shadow copy.
+ * Arithmetic in torch's order: p*=(1-lr·wd); m=lerp(m,g,1-β1); v=β2·v+(1-β2)g²;
+ * p -= step_size · m / (sqrt(v)/bc2_sqrt + eps), step_size = lr/(1-β1^t), bc2_sqrt = sqrt(1-β2^t). */
+int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
+                    float beta1, float beta2, float eps, float weight_decay, float step_size,
+                    float bc2_sqrt, void* stream);
+/* bf16 shadow copy of fp32 values: dst[i] = bf16(src[i]). */
+int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream);
+/* y[i] += x[i] (f32), used to accumulate gradients across backward calls. */
+int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Whole-model executor.  The caller owns every buffer; ergm_model_plan only records pointers and
+ * dimensions (see ergm_amd/model.py for the layout it builds).  Forward = src/model.py:654-737;
+ * backward = loss.backward() (src/main.py:154), with per-layer entry points so a data-parallel
+ * caller can start gradient all-reduce buckets as layers finish.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct ergm_model_plan ergm_model_plan;
+
+typedef struct {
+    int vocab, vocab_pad, n_embd, n_layer, n_head, n_inner, n_positions;
+    int batch, seq;           /* local (per-rank) batch and sequence length */
+    float eps;
+    int has_features;         /* visual/audio injection present */
+    int ld_vis;               /* row stride of the visual feature (Tv*E when [B,Tv,E]) */
+} ergm_model_dims;
+
+/* Pointer table: names follow the reference state_dict; see ergm_amd/model.py. */
+typedef struct {
+    /* fp32 master params and their bf16 shadows (same element offsets) */
+    const float* wte;  const void* wte_b;   /* [vocab_pad][E] */
+    const float* wpe;                        /* [n_positions][E] */
+    const float* ln_f_w; const float* ln_f_b;
+    const float* emo_w;                      /* [7][E] */
+    const void* capkv_w_b; const float* capkv_b;  /* stacked cross c_attn: [E][L*2E], [L*2E] */
+    /* per layer i, base pointers into the flat buffers; offsets of each tensor within a layer
+     * block are given by layer_off[] (elements) in the order of ergm_layer_tensor. */
+    const float* layer_f32; const void* layer_b16;
+    int64_t layer_stride;     /* elements between layer i and i+1 blocks (negative: reversed order) */
+    int64_t layer_off[18];
+    /* gradients (f32, same layout as params) */
+    float* g_wte; float* g_wpe; float* g_ln_f_w; float* g_ln_f_b; float* g_emo_w;
+    float* g_capkv_w; float* g_capkv_b; float* g_layer;
+} ergm_model_params;
+
+typedef enum {
+    ERGM_T_LN1_W = 0, ERGM_T_LN1_B, ERGM_T_ATTN_W, ERGM_T_ATTN_B, ERGM_T_APROJ_W, ERGM_T_APROJ_B,
+    ERGM_T_LNX_W, ERGM_T_LNX_B, ERGM_T_XQ_W, ERGM_T_XQ_B, ERGM_T_XPROJ_W, ERGM_T_XPROJ_B,
+    ERGM_T_LN2_W, ERGM_T_LN2_B, ERGM_T_FC_W, ERGM_T_FC_B, ERGM_T_MPROJ_W, ERGM_T_MPROJ_B,
+} ergm_layer_tensor;
+
+/* Bytes of device workspace the executor needs (activations saved for backward + scratch). */
+size_t ergm_model_workspace_size(const ergm_model_dims* dims);
+int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* workspace,
+                      size_t ws_bytes, ergm_model_plan** out_plan);
+int ergm_model_destroy(ergm_model_plan* plan);
+/* Inputs for the next forward (device pointers, int64 [B][S]; features f32 or NULL; labels may be
+ * NULL for inference).  n_valid_global: device int the caller filled (ergm_count_valid +
+ * optional all-reduce); B_global: global batch for the emotion-loss mean.                       */
+int ergm_model_set_inputs(ergm_model_plan* plan, const int64_t* ids, const int64_t* tt,
+                          const int64_t* cap_ids, const float* vis, const float* aud,
+                          const int64_t* labels, const int64_t* emotion_labels,
+                          const int* n_valid_global, int B_global);
+/* Forward. Outputs (device): logits bf16 [B*S][vocab_pad], emotion logits f32 [B][7],
+ * loss parts f32 (ergm_loss_finalize layout: [lm, emotion, total], local contributions over the
+ * global normalisers); with `train`, dlogits are prepared for the backward.                      */
+int ergm_model_forward(ergm_model_plan* plan, void* logits, float* emo_logits, float* out_loss,
+                       int train, void* stream);
+/* Backward in stages so a DP caller can overlap communication:
+ *   ergm_model_backward_head  — LM head + emotion head + ln_f (grads of wte(part), emo, ln_f)
+ *   ergm_model_backward_layer — block `layer` (call for L-1 … 0)
+ *   ergm_model_backward_embed — stacked caption K/V projection + embeddings (wte rest, wpe)   */
+int ergm_model_backward_head(ergm_model_plan* plan, const float* grad_scale_dev, void* stream);
+int ergm_model_backward_layer(ergm_model_plan* plan, int layer, void* stream);
+int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
+
+/* Library information and errors. */
+int ergm_version(void);
+int ergm_last_error(char* buf, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ERGM_HIP_H */

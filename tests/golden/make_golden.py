@@ -1,0 +1,224 @@
+"""Generate the golden fixtures that pin ``oracle/gpt2_oracle.py`` to the reference.
+
+Runs ONLY in the build container (needs ``/root/reference``).  It imports the reference model
+(``/root/reference/src/model.py``) through the loader shim of SURVEY.md §8(c) — no source edits,
+bytecode writing disabled — loads seeded weights with ``load_state_dict(strict=True)``, runs the
+training-mode forward + backward exactly as the only runnable reference call does (with
+``caption_ids``), checks the oracle restatement against it, and writes the reference's own outputs
+as ``tests/golden/*.npz``.  Also pins the AdamW / LR-schedule restatement against
+``torch.optim.AdamW`` + ``transformers.get_polynomial_decay_schedule_with_warmup`` (the third-party
+code src/main.py:68,93-95 calls).
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import gpt2_oracle as O  # noqa: E402
+from ergm_amd.data import synthetic_batch  # noqa: E402
+
+REF_SRC = "/root/reference/src"
+
+
+def load_reference():
+    """Loader shim: stub 4 names removed from transformers 5.x, 4.26 get_head_mask
+    semantics, map the hard-coded ``.to("cuda")`` (src/model.py:401-408) to CPU, dict tied keys."""
+    import torch.nn as nn
+    import transformers.modeling_utils as mu
+    import transformers.pytorch_utils as pu
+    if not hasattr(mu, "SequenceSummary"):
+        mu.SequenceSummary = object
+    for n in ("find_pruneable_heads_and_indices", "prune_conv1d_layer"):
+        if not hasattr(pu, n):
+            setattr(pu, n, lambda *a, **k: None)
+    m = types.ModuleType("transformers.utils.model_parallel_utils")
+    m.assert_device_map = lambda *a, **k: None
+    m.get_device_map = lambda *a, **k: None
+    sys.modules["transformers.utils.model_parallel_utils"] = m
+    mu.PreTrainedModel.get_head_mask = lambda self, hm, n, *a, **k: [None] * n
+    if not getattr(nn.Module.to, "_ergm_shim", False):
+        _to = nn.Module.to
+
+        def _to_cpu(self, *a, **k):
+            a = tuple("cpu" if isinstance(x, str) and x.startswith("cuda") else x for x in a)
+            return _to(self, *a, **k)
+        _to_cpu._ergm_shim = True
+        nn.Module.to = _to_cpu
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    import model as refmodel  # the reference's src/model.py
+    refmodel.GPT2LMHeadModel._tied_weights_keys = {"lm_head.weight": "transformer.wte.weight"}
+    return refmodel
+
+
+def ref_run(refmodel, cfg: O.OracleConfig, P, batch):
+    from transformers import GPT2Config
+    gcfg = GPT2Config(vocab_size=cfg.vocab_size, n_embd=cfg.n_embd, n_layer=cfg.n_layer,
+                      n_head=cfg.n_head, n_positions=cfg.n_positions, n_inner=cfg.n_inner,
+                      attn_pdrop=0.0, resid_pdrop=0.0, embd_pdrop=0.0,
+                      layer_norm_epsilon=cfg.layer_norm_epsilon)
+    net = refmodel.GPT2LMHeadModel(gcfg)
+    sd = dict(P)
+    sd["lm_head.weight"] = P["transformer.wte.weight"]
+    net.load_state_dict(sd, strict=True)
+    assert net.lm_head.weight.data_ptr() == net.transformer.wte.weight.data_ptr(), "lm_head not tied"
+    net.train()
+    kw = dict(input_ids=batch["input_ids"], token_type_ids=batch["token_type_ids"],
+              labels=batch["labels"], emotion_labels=batch["emotion_labels"],
+              caption_ids=batch["caption_ids"])
+    if batch.get("visual_feat") is not None:
+        kw["imgs"] = batch["visual_feat"]       # [B, Tv, E]: imgs[i][0] is row 0 (src/model.py:497)
+        kw["auds"] = batch["audio_feat"]        # [B, E] (src/model.py:498)
+    out = net(**kw)
+    out.loss.backward()
+    grads = {}
+    for name, p in net.named_parameters():
+        grads[name] = p.grad.detach().clone()
+    # lm_head is tied: its grad is folded into wte's (named_parameters yields the shared tensor once)
+    return out, grads
+
+
+def compare(tag, a, b, rtol):
+    a, b = a.double(), b.double()
+    err = (a - b).norm() / max(b.norm().item(), 1e-30)
+    ok = err.item() <= rtol
+    print(f"  {tag:55s} rel-L2 {err.item():.3e} {'ok' if ok else 'FAIL'}")
+    return ok
+
+
+def build_case(refmodel, name, cfg, B, S, seed, with_features=True, visual_rows=1, n_turns=5,
+               full_grads=True, vocab_hi=None):
+    print(f"[{name}] L={cfg.n_layer} E={cfg.n_embd} H={cfg.n_head} V={cfg.vocab_size} B={B} S={S}")
+    P = O.init_params(cfg, seed=seed)
+    vhi = vocab_hi if vocab_hi is not None else cfg.vocab_size - 3
+    batch = synthetic_batch(B, S, n_turns=n_turns, feat_dim=cfg.n_embd, seed=seed + 1000,
+                            vocab_hi=vhi, visual_rows=visual_rows, with_features=with_features,
+                            sp1=cfg.vocab_size - 2, sp2=cfg.vocab_size - 1, eos=vhi - 1)
+    ref_out, ref_g = ref_run(refmodel, cfg, P, batch)
+    ora_out, ora_g = O.loss_and_grads(P, cfg, batch)
+    ok = True
+    ok &= compare("loss", ora_out["loss"].reshape(1), ref_out.loss.detach().reshape(1), 1e-5)
+    ok &= compare("logits", ora_out["logits"], ref_out.logits.detach(), 1e-5)
+    ok &= compare("emotion_logits", ora_out["emotion_logits"], ref_out.emotion_logits.detach(), 1e-5)
+    for k in ora_g:
+        ok &= compare("grad " + k, ora_g[k], ref_g[k], 1e-4)
+    assert ok, f"oracle does not match the reference on {name}"
+    rec = {
+        "config": np.array([cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_positions],
+                           dtype=np.int64),
+        "seed": np.array(seed),
+        "loss": ref_out.loss.detach().numpy(),
+        "loss_lm": ora_out["loss_lm"].numpy(),
+        "loss_emotion": ora_out["loss_emotion"].numpy(),
+        "emotion_logits": ref_out.emotion_logits.detach().numpy(),
+    }
+    for k, v in batch.items():
+        rec["in_" + k] = v.numpy()
+    logits = ref_out.logits.detach()
+    if logits.numel() <= 200_000:
+        rec["logits"] = logits.numpy()
+    else:
+        rec["logits_head"] = logits[:, :4, :64].numpy().copy()
+        rec["logits_tail"] = logits[:, -2:, -64:].numpy().copy()
+        rec["logits_rowsum"] = logits.sum(-1).numpy()
+    for k, g in ref_g.items():
+        if full_grads:
+            rec["grad:" + k] = g.numpy()
+        else:
+            rec["gradnorm:" + k] = np.array(g.double().norm().item())
+            rec["gradhead:" + k] = g.reshape(-1)[:32].numpy().copy()
+    return P, batch, rec
+
+
+def adamw_case():
+    """Two AdamW steps under the poly-decay schedule vs torch.optim.AdamW + transformers schedule."""
+    from transformers import get_polynomial_decay_schedule_with_warmup
+    g = torch.Generator().manual_seed(7)
+    shapes = {"a": (33, 17), "b": (64,)}
+    P = {k: torch.randn(s, generator=g) for k, s in shapes.items()}
+    grads = [{k: torch.randn(s, generator=g) for k, s in shapes.items()} for _ in range(3)]
+    lr, warm, total = 2e-5, 1, 5
+    tp = {k: torch.nn.Parameter(v.clone()) for k, v in P.items()}
+    opt = torch.optim.AdamW(list(tp.values()), lr=lr, foreach=False)
+    sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=warm, num_training_steps=total,
+                                                      power=2)
+    lrs = []
+    for G in grads:
+        for k, p in tp.items():
+            p.grad = G[k].clone()
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sched.step()
+    st = O.AdamWState()
+    mine = {k: v.clone() for k, v in P.items()}
+    my_lrs = []
+    for i, G in enumerate(grads):
+        cur = O.poly_decay_lr(i, lr, warm, total)
+        my_lrs.append(cur)
+        O.adamw_step(mine, G, st, cur)
+    assert np.allclose(lrs, my_lrs, rtol=1e-12, atol=0), (lrs, my_lrs)
+    for k in P:
+        assert torch.allclose(mine[k], tp[k].detach(), rtol=1e-6, atol=1e-9), k
+    # the schedule over a longer horizon (warmup 10%, as src/main.py:91 default warmup_ratio=0.1)
+    lr2, total2 = 2e-5, 40
+    warm2 = int(0.1 * total2)
+    opt2 = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=lr2)
+    s2 = get_polynomial_decay_schedule_with_warmup(opt2, num_warmup_steps=warm2, num_training_steps=total2,
+                                                   power=2)
+    ref_lrs = []
+    for _ in range(total2 + 3):
+        ref_lrs.append(opt2.param_groups[0]["lr"])
+        opt2.step()
+        s2.step()
+    print("  adamw + schedule restatement ok")
+    rec = {"lrs": np.array(lrs), "sched_lrs": np.array(ref_lrs),
+           "sched_args": np.array([lr2, warm2, total2])}
+    for k in P:
+        rec["p0:" + k] = P[k].numpy()
+        rec["p3:" + k] = tp[k].detach().numpy()
+        for i, G in enumerate(grads):
+            rec[f"g{i}:" + k] = G[k].numpy()
+    return rec
+
+
+def main():
+    torch.manual_seed(0)
+    refmodel = load_reference()
+    out_dir = HERE
+    # 1. tiny, single head (d=64), full grads + one AdamW step: the byte-level fixture
+    cfg = O.OracleConfig(vocab_size=256, n_embd=64, n_layer=2, n_head=1, n_positions=64)
+    P, batch, rec = build_case(refmodel, "tiny_e64", cfg, B=2, S=32, seed=11)
+    np.savez_compressed(os.path.join(out_dir, "tiny_e64.npz"), **rec)
+    # 2. two heads, vocab not a multiple of 64, 4 visual rows (row 0 used), B=3
+    cfg = O.OracleConfig(vocab_size=500, n_embd=128, n_layer=2, n_head=2, n_positions=128)
+    _, _, rec = build_case(refmodel, "small_e128_v500", cfg, B=3, S=64, seed=22, visual_rows=4,
+                           full_grads=False)
+    np.savez_compressed(os.path.join(out_dir, "small_e128_v500.npz"), **rec)
+    # 3. C1 shape: GPT-2-small text-only, B=2, S=128 (BASELINE configs[0]); stats only
+    cfg = O.OracleConfig()
+    _, _, rec = build_case(refmodel, "c1_gpt2small_textonly", cfg, B=2, S=128, seed=33,
+                           with_features=False, full_grads=False, vocab_hi=50257)
+    np.savez_compressed(os.path.join(out_dir, "c1_gpt2small_textonly.npz"), **rec)
+    # 4. GPT-2-small + fusion, MELD shape, B=2 S=128 (a C2-shaped slice); stats only
+    _, _, rec = build_case(refmodel, "c2slice_gpt2small_fusion", cfg, B=2, S=128, seed=44,
+                           full_grads=False, vocab_hi=50257)
+    np.savez_compressed(os.path.join(out_dir, "c2slice_gpt2small_fusion.npz"), **rec)
+    np.savez_compressed(os.path.join(out_dir, "adamw_sched.npz"), **adamw_case())
+    print("golden fixtures written to", out_dir)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,295 @@
+"""Per-kernel parity on the GPU: every HIP kernel against a plain PyTorch fp32/fp64 reference of the
+same op on the same (seeded) inputs, called through the C-ABI (ergm_amd.ops → libergm_hip.so)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ergm_amd import _lib as L
+from ergm_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _mat(A, layout_rowK, M, K):
+    """logical [M,K] from storage"""
+    return A.float() if layout_rowK else A.float().t()
+
+
+GEMM_SHAPES = [(256, 256, 128), (2048, 2304, 768), (2048, 768, 3072), (96, 200, 72), (64, 50304, 128),
+               (768, 768, 2048), (200, 96, 1024), (8, 24, 16)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("al,bl", [(L.MK, L.NK), (L.MK, L.KN), (L.KM, L.NK), (L.KM, L.KN)])
+def test_gemm_layouts(gpu, M, N, K, al, bl):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K + al * 2 + bl)
+    Am = torch.randn(M, K, generator=g)
+    Bm = torch.randn(K, N, generator=g)
+    A = _bf(Am if al == L.MK else Am.t().contiguous()).to(gpu)
+    B = _bf(Bm.t().contiguous() if bl == L.NK else Bm).to(gpu)
+    ref = _bf(Am).double() @ _bf(Bm).double()
+    out = ops.gemm(A, B, M, N, K, al, bl, out_dtype=torch.float32)
+    assert _rel(out.cpu(), ref) < 1e-5
+    outb = ops.gemm(A, B, M, N, K, al, bl, out_dtype=torch.bfloat16)
+    assert _rel(outb.float().cpu(), ref) < 6e-3
+
+
+@pytest.mark.parametrize("split", [2, 3, 5])
+def test_gemm_split_k(gpu, split):
+    M, N, K = 192, 320, 2048
+    A = torch.randn(M, K, device=gpu).bfloat16()
+    B = torch.randn(N, K, device=gpu).bfloat16()
+    ref = A.double() @ B.double().t()
+    out = ops.gemm(A, B, M, N, K, L.MK, L.NK, split_k=split)
+    assert _rel(out, ref) < 1e-5
+    # split-K is deterministic: same result twice, bit for bit
+    out2 = ops.gemm(A, B, M, N, K, L.MK, L.NK, split_k=split)
+    assert torch.equal(out, out2)
+
+
+def test_gemm_epilogues(gpu):
+    M, N, K = 256, 384, 192
+    A = torch.randn(M, K, device=gpu).bfloat16()
+    W = (0.1 * torch.randn(K, N, device=gpu)).bfloat16()  # Conv1D weight [in, out]
+    bias = torch.randn(N, device=gpu)
+    acc = A.double() @ W.double()
+    # bias
+    out = ops.gemm(A, W, M, N, K, L.MK, L.KN, epilogue=L.EPI_BIAS, bias=bias)
+    assert _rel(out, acc + bias.double()) < 1e-5
+    # bias + gelu_new with pre-activation side output
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    act = ops.gemm(A, W, M, N, K, L.MK, L.KN, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_GELU, bias=bias,
+                   aux_out=pre)
+    z = (acc + bias.double()).float()
+    gelu = 0.5 * z * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (z + 0.044715 * torch.pow(z, 3.0))))
+    assert _rel(pre.float(), z) < 6e-3
+    assert _rel(act.float(), gelu) < 6e-3
+    # residual add (in place)
+    res = torch.randn(M, N, device=gpu)
+    expect = res.double() + acc + bias.double()
+    ops.gemm(A, W, M, N, K, L.MK, L.KN, out=res, epilogue=L.EPI_BIAS_RESID, bias=bias, aux=res)
+    assert _rel(res, expect) < 1e-6
+    # gelu backward: v * gelu'(pre)
+    x = pre.float().requires_grad_(True)
+    y = 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
+    y.backward(acc.float())
+    out = ops.gemm(A, W, M, N, K, L.MK, L.KN, out_dtype=torch.float32, epilogue=L.EPI_GELU_BWD, aux=pre)
+    assert _rel(out, x.grad) < 1e-5
+    # accumulate + device alpha
+    base = torch.randn(M, N, device=gpu)
+    alpha = torch.tensor([0.5], device=gpu)
+    expect = base.double() + 0.5 * acc
+    ops.gemm(A, W, M, N, K, L.MK, L.KN, out=base, epilogue=L.EPI_ACCUM, alpha_dev=alpha)
+    assert _rel(base, expect) < 1e-6
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 128
+    A = torch.eye(n, device=gpu).bfloat16()
+    B = torch.arange(n * n, device=gpu, dtype=torch.float32).reshape(n, n).remainder(97).bfloat16()
+    for bl, Bs in ((L.KN, B), (L.NK, B.t().contiguous())):
+        out = ops.gemm(A, Bs, n, n, n, L.MK, bl)
+        assert torch.equal(out, B.float())
+
+
+def test_gemm_rejects_bad_args(gpu):
+    A = torch.randn(64, 60, device=gpu).bfloat16()
+    with pytest.raises(ValueError):
+        ops.gemm(A, A, 64, 64, 60, L.MK, L.NK)  # K % 8 != 0
+
+
+def _attn_ref(q, k, v, causal):
+    w = torch.matmul(q, k.transpose(-1, -2)) / 8.0
+    if causal:
+        S = q.shape[-2]
+        mask = torch.tril(torch.ones(S, S, dtype=torch.bool, device=q.device))
+        w = torch.where(mask, w, torch.finfo(w.dtype).min)
+    p = torch.softmax(w, -1)
+    return p @ v
+
+
+@pytest.mark.parametrize("B,H,S,causal", [(2, 12, 128, True), (2, 12, 128, False), (1, 2, 512, True),
+                                          (3, 1, 32, True), (2, 4, 100, False), (2, 2, 72, True)])
+def test_attention_fwd_bwd(gpu, B, H, S, causal):
+    E = 64 * H
+    torch.manual_seed(B * 1000 + S + H)
+    qkv = torch.randn(B * S, 3 * E, device=gpu).bfloat16()
+    q, k, v = qkv[:, :E], qkv[:, E:2 * E], qkv[:, 2 * E:]
+    o, lse = ops.attn_fwd(q, k, v, B, H, S, S, causal)
+
+    def heads(t):
+        return t.float().reshape(B, S, H, 64).permute(0, 2, 1, 3)
+    qf, kf, vf = (heads(t).requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qf, kf, vf, causal)
+    got = o.float().reshape(B, S, H, 64).permute(0, 2, 1, 3)
+    assert _rel(got, ref.detach()) < 8e-3
+    w = torch.matmul(qf, kf.transpose(-1, -2)) / 8.0
+    if causal:
+        w = w.masked_fill(~torch.tril(torch.ones(S, S, dtype=torch.bool, device=gpu)), float("-inf"))
+    assert _rel(lse, torch.logsumexp(w, -1).detach()) < 1e-4
+    dout = torch.randn(B * S, E, device=gpu).bfloat16()
+    ref.backward(heads(dout))
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, dout, lse, B, H, S, S, causal)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        assert _rel(heads(got), want) < 2e-2
+
+
+def test_attention_cross_strided(gpu):
+    """Cross-attention reading K/V straight out of a stacked [T, L*2E] projection buffer."""
+    B, H, S, Lyr = 2, 4, 128, 3
+    E = 64 * H
+    q = torch.randn(B * S, E, device=gpu).bfloat16()
+    kv_all = torch.randn(B * S, Lyr * 2 * E, device=gpu).bfloat16()
+    l = 1
+    k = kv_all[:, l * 2 * E: l * 2 * E + E]
+    v = kv_all[:, l * 2 * E + E: (l + 1) * 2 * E]
+    o, lse = ops.attn_fwd(q, k, v, B, H, S, S, False)
+
+    def heads(t):
+        return t.float().reshape(B, S, H, 64).permute(0, 2, 1, 3)
+    ref = _attn_ref(heads(q), heads(k), heads(v), False)
+    assert _rel(heads(o), ref) < 8e-3
+
+
+@pytest.mark.parametrize("rows,E", [(2048, 768), (100, 1024), (64, 64), (33, 128)])
+def test_layernorm(gpu, rows, E):
+    torch.manual_seed(rows + E)
+    x = (torch.randn(rows, E, device=gpu) * 3 + 1).requires_grad_(True)
+    gm = (1 + 0.1 * torch.randn(E, device=gpu)).requires_grad_(True)
+    bt = (0.1 * torch.randn(E, device=gpu)).requires_grad_(True)
+    y, mean, rstd = ops.layernorm_fwd(x.detach(), gm.detach(), bt.detach())
+    ref = F.layer_norm(x, (E,), gm, bt, 1e-5)
+    assert _rel(y.float(), ref.detach()) < 6e-3
+    dy = torch.randn(rows, E, device=gpu)
+    ref.backward(dy)
+    dres0 = torch.randn(rows, E, device=gpu)
+    dres, dres_b, dg, db = ops.layernorm_bwd(dy, x.detach(), mean, rstd, gm.detach(), dres0.clone())
+    assert _rel(dres - dres0, x.grad) < 1e-5
+    assert _rel(dres_b.float(), dres) < 6e-3
+    assert _rel(dg, gm.grad) < 1e-5
+    assert _rel(db, bt.grad) < 1e-5
+
+
+@pytest.mark.parametrize("rows,cols,dt", [(2048, 768, torch.float32), (2048, 2304, torch.bfloat16),
+                                          (16, 98304, torch.float32), (130, 64, torch.bfloat16)])
+def test_colsum(gpu, rows, cols, dt):
+    X = torch.randn(rows, cols, device=gpu).to(dt)
+    out = ops.colsum(X)
+    assert _rel(out, X.double().sum(0)) < 1e-6
+    out2 = ops.colsum(X, out=out.clone(), accumulate=True)
+    assert _rel(out2, 2 * X.double().sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("with_feat", [True, False])
+def test_embedding_fwd_bwd(gpu, with_feat):
+    B, S, E, V = 4, 64, 256, 1000
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, V - 3, (B, S), generator=g)
+    ids[0, :10] = 7  # collisions
+    tt = torch.where(torch.arange(S) < 30, V - 2, V - 1).expand(B, S).contiguous()
+    cap = torch.randint(0, V - 3, (B, S), generator=g)
+    cap[1, :5] = 7
+    wte = torch.randn(V, E, generator=g)
+    wpe = torch.randn(128, E, generator=g)
+    vis = torch.randn(B, 3, E, generator=g) if with_feat else None
+    aud = torch.randn(B, E, generator=g) if with_feat else None
+    dev = lambda t: None if t is None else t.to(gpu)
+    h0, capb = ops.embed_fwd(dev(ids), dev(tt), dev(cap), dev(wte), dev(wpe), dev(vis), dev(aud))
+    wt = wte.clone().requires_grad_(True)
+    wp = wpe.clone().requires_grad_(True)
+    emb = F.embedding(ids, wt)
+    if with_feat:
+        add = torch.zeros_like(emb)
+        add[:, 0] = vis[:, 0]
+        add[:, 1] = aud
+        emb = emb + add
+    ref = emb + F.embedding(torch.arange(S), wp) + F.embedding(tt, wt)
+    cref = F.embedding(cap, wt)
+    assert _rel(h0.cpu(), ref.detach().reshape(B * S, E)) < 1e-7
+    assert _rel(capb.float().cpu(), cref.detach().reshape(B * S, E)) < 6e-3
+    dh = torch.randn(B * S, E, generator=g)
+    dc = torch.randn(B * S, E, generator=g)
+    (ref.reshape(B * S, E) * dh).sum().backward(retain_graph=True)
+    (cref.reshape(B * S, E) * dc).sum().backward()
+    base = torch.randn(V, E, generator=g)
+    dwte = dev(base.clone())
+    dwpe = torch.zeros(128, E, device=gpu)
+    ops.embed_bwd(dev(ids), dev(tt), dev(cap), dev(dh), dev(dc), dwte, dwpe)
+    assert _rel(dwte.cpu() - base, wt.grad) < 1e-6
+    assert _rel(dwpe.cpu(), wp.grad) < 1e-6
+    # deterministic: bitwise identical on a second run
+    dwte2 = dev(base.clone())
+    ops.embed_bwd(dev(ids), dev(tt), dev(cap), dev(dh), dev(dc), dwte2, dwpe)
+    assert torch.equal(dwte, dwte2)
+
+
+@pytest.mark.parametrize("B,S,V,ldl", [(4, 128, 50260, 50304), (2, 16, 500, 512), (3, 33, 256, 256)])
+def test_cross_entropy(gpu, B, S, V, ldl):
+    g = torch.Generator().manual_seed(V)
+    logits = torch.zeros(B * S, ldl)
+    logits[:, :V] = 3 * torch.randn(B * S, V, generator=g)
+    logits[:, V:] = 1e4  # padding columns must be ignored
+    lb = _bf(logits)
+    labels = torch.randint(0, V, (B, S), generator=g)
+    labels[:, : S // 2] = -100
+    n = ops.count_valid(labels.to(gpu))
+    rl, dl = ops.xent(lb.to(gpu), labels.to(gpu), n, V)
+    x = lb[:, :V].float().reshape(B, S, V)[:, :-1].reshape(-1, V).requires_grad_(True)
+    y = labels[:, 1:].reshape(-1)
+    loss = F.cross_entropy(x, y, ignore_index=-100)
+    loss.backward()
+    assert int(n.item()) == int((y != -100).sum())
+    assert abs(rl.sum().item() / n.item() - loss.item()) < 1e-4 * max(1.0, loss.item())
+    got = dl.float().cpu().reshape(B, S, ldl)
+    assert torch.all(got[:, -1] == 0) and torch.all(got[:, :, V:] == 0)
+    assert _rel(got[:, :-1, :V].reshape(-1, V), x.grad) < 6e-3
+
+
+def test_emotion_head(gpu):
+    B, S, E, Cn = 16, 8, 768, 7
+    h = torch.randn(B * S, E, device=gpu).bfloat16()
+    W = 0.02 * torch.randn(Cn, E, device=gpu)
+    labels = torch.randint(0, Cn, (B,), device=gpu)
+    dh = torch.zeros(B * S, E, device=gpu)
+    gs = torch.tensor([2.0], device=gpu)
+    logits, loss_sum, dW = ops.emotion_head(h, W, labels, B, S, dh=dh, grad_scale=gs)
+    hl = h.float().reshape(B, S, E)[:, -1].clone().requires_grad_(True)
+    Wr = W.clone().requires_grad_(True)
+    ref = hl @ Wr.t()
+    loss = F.cross_entropy(ref, labels)
+    (2.0 * loss).backward()
+    assert _rel(logits, ref.detach()) < 1e-5
+    assert abs(loss_sum.item() / B - loss.item()) < 1e-5
+    assert _rel(dW, Wr.grad) < 1e-5
+    assert _rel(dh.reshape(B, S, E)[:, -1], hl.grad) < 1e-5
+    assert torch.all(dh.reshape(B, S, E)[:, :-1] == 0)
+
+
+def test_adamw_matches_oracle(gpu):
+    from oracle import gpt2_oracle as O
+    n = 4096 + 64
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) for _ in range(3)]
+    P = {"x": p0.clone()}
+    st = O.AdamWState()
+    p, m, v = p0.clone().to(gpu), torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    for i, G in enumerate(grads):
+        lr = O.poly_decay_lr(i, 2e-5, 1, 5) + 1e-3
+        O.adamw_step(P, {"x": G}, st, lr)
+        ops.adamw_step(p, G.to(gpu), m, v, pb, lr, 0.9, 0.999, 1e-8, 0.01, i + 1)
+    assert torch.allclose(p.cpu(), P["x"], rtol=2e-6, atol=1e-7)
+    assert torch.equal(pb.cpu(), p.cpu().bfloat16())
