@@ -59,7 +59,7 @@ _SIGS = {
     "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),
     "ergm_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, f32, vp]),
     "ergm_layernorm_bwd_workspace_size": (sz, [i32, i32]),
-    "ergm_layernorm_bwd": (i32, [vp] * 11 + [sz, i32, i32, vp]),
+    "ergm_layernorm_bwd": (i32, [vp] * 10 + [sz, i32, i32, vp]),
     "ergm_colsum_workspace_size": (sz, [i32, i32]),
     "ergm_colsum": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
     "ergm_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),

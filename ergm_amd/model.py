@@ -1,0 +1,277 @@
+"""Drop-in ``GPT2LMHeadModel`` of ERGM, running the fused HIP training step on MI355X.
+
+Mirrors the reference interface (src/model.py:599-737):
+
+* ``GPT2LMHeadModel(config)`` with the reference's state_dict names (``transformer.h.{i}...``,
+  tied ``lm_head.weight``, ``emotion_head.weight``) so checkpoints interchange;
+* ``forward(input_ids, token_type_ids=, labels=, emotion_labels=, imgs=, auds=, caption_ids=)``
+  (plus the build's aliases ``visual_feat=`` / ``audio_feat=``) returning an object with ``.loss``,
+  ``.logits`` [B,S,V] and ``.emotion_logits`` [B,7] (``CausalLMOutputWithEmotionClassification``,
+  src/model.py:48-60);
+* ``loss.backward()`` fills the parameter gradients; ``torch.optim.AdamW(model.parameters())`` works
+  unchanged, and ``ergm_amd.optim.FusedAdamW`` runs the same update as one HIP kernel.
+
+Storage (see params.py): one fp32 ``nn.Parameter`` holding every weight, a bf16 shadow read by the
+MFMA GEMMs, one fp32 gradient buffer.  The whole forward is one native call and the backward three
+native stages per step (ergm_model_* in include/ergm_hip.h); there is no CPU fallback.
+
+Differences from the reference, by design: dropout is not supported (the parity path runs p=0);
+``logits`` come back as bf16 (the compute dtype) and are not differentiable (the reference trainer
+only back-propagates ``loss``); the KV-cache / ``past_key_values``, ``attention_mask``,
+``head_mask``, ``inputs_embeds`` and ``output_attentions`` paths are not part of the training hot
+path and raise ``NotImplementedError``.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .config import ERGMConfig, NUM_EMOTIONS
+from .params import build_layout, state_dict_names
+from .runtime import ModelRunner
+
+
+@dataclass
+class CausalLMOutputWithEmotionClassification:
+    """src/model.py:48-60 (fields the training path produces)."""
+    loss: Optional[torch.Tensor] = None
+    logits: Optional[torch.Tensor] = None
+    emotion_logits: Optional[torch.Tensor] = None
+    past_key_values: Optional[tuple] = None
+    hidden_states: Optional[tuple] = None
+    attentions: Optional[tuple] = None
+    cross_attentions: Optional[tuple] = None
+    loss_lm: Optional[torch.Tensor] = None        # build extra: the LM part (PPL = exp(loss_lm))
+    loss_emotion: Optional[torch.Tensor] = None   # build extra: the emotion CE part
+
+    def __getitem__(self, i):
+        return (self.loss, self.logits, self.emotion_logits)[i]
+
+
+def _as_config(config) -> ERGMConfig:
+    if isinstance(config, ERGMConfig):
+        return config
+    g = lambda k, d=None: getattr(config, k, d)  # noqa: E731  (transformers GPT2Config)
+    return ERGMConfig(vocab_size=g("vocab_size"), n_embd=g("n_embd"), n_layer=g("n_layer"), n_head=g("n_head"),
+                      n_positions=g("n_positions", 1024), n_inner=g("n_inner"),
+                      layer_norm_epsilon=g("layer_norm_epsilon", 1e-5),
+                      initializer_range=g("initializer_range", 0.02))
+
+
+class _FusedTrainStep(torch.autograd.Function):
+    """Autograd bridge: forward = one native forward; backward = native backward stages writing
+    straight into the flat gradient buffer (returned grad for ``flat`` is None: the buffer is
+    installed as ``flat.grad`` directly, avoiding an extra 600 MB accumulate pass per step)."""
+
+    @staticmethod
+    def forward(ctx, flat, model, runner, ids, tt, cap_ids, vis, aud, labels, emo_labels):
+        logits, emo, loss = runner.forward(ids, tt, cap_ids, vis, aud, labels, emo_labels, train=True)
+        ctx.model, ctx.runner = model, runner
+        ctx.mark_non_differentiable(logits, emo)
+        ctx.set_materialize_grads(False)
+        return loss, logits, emo
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_logits, grad_emo):
+        if grad_logits is not None or grad_emo is not None:
+            raise NotImplementedError("gradients through logits / emotion_logits are not supported; "
+                                      "back-propagate the loss")
+        model, runner = ctx.model, ctx.runner
+        flat = model.flat
+        gl = grad_loss
+        if gl is not None:
+            gl = gl.reshape(-1)[2:3] if gl.numel() == 3 else gl.reshape(1)
+            gl = gl.float().contiguous()
+        if flat.grad is None:
+            runner.backward(gl)                      # writes model.grad_buf
+            flat.grad = model.grad_buf
+        else:
+            # accumulate semantics when the caller did not zero the gradient
+            if flat.grad.data_ptr() == model.grad_buf.data_ptr():
+                tmp = model._grad_tmp()
+                tmp.copy_(model.grad_buf)            # the gradient accumulated so far
+                runner.backward(gl)                  # overwrites grad_buf with this backward's
+                ops.axpy(tmp, model.grad_buf)
+            else:
+                runner.backward(gl)
+                ops.axpy(model.grad_buf, flat.grad)
+        return (None,) * 10
+
+
+class GPT2LMHeadModel(nn.Module):
+    num_emotions = NUM_EMOTIONS
+
+    def __init__(self, config, device=None, process_group=None):
+        super().__init__()
+        cfg = _as_config(config)
+        cfg.validate()
+        if cfg.head_dim != 64:
+            raise ValueError(f"head_dim must be 64 for the fused attention kernels (got {cfg.head_dim})")
+        self.config = cfg
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.layout = build_layout(cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.inner, cfg.n_positions)
+        n = self.layout.total
+        self.flat = nn.Parameter(torch.zeros(n, dtype=torch.float32, device=dev))
+        self.register_buffer("flat_b16", torch.zeros(n, dtype=torch.bfloat16, device=dev), persistent=False)
+        self.grad_buf = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._tmp = None
+        self._runners: Dict[tuple, ModelRunner] = {}
+        self._b16_version = -1
+        self.process_group = process_group
+        self.init_weights()
+
+    # ---- parameters / state_dict ---------------------------------------------------------
+    def view(self, name: str, t: Optional[torch.Tensor] = None) -> torch.Tensor:
+        v = self.layout.views[name]
+        t = self.flat.data if t is None else t
+        return t.as_strided(v.shape, v.stride, v.offset)
+
+    def init_weights(self, seed: Optional[int] = None) -> None:
+        """``_init_weights`` (src/model.py:359-375): N(0, 0.02) matrices and embeddings, c_proj
+        N(0, 0.02/sqrt(2L)), LayerNorm 1/0, biases 0; padding rows zero."""
+        cfg = self.config
+        g = torch.Generator(device="cpu")
+        g.manual_seed(0 if seed is None else seed)
+        sd = {}
+        for name in state_dict_names(self.layout):
+            if name == "lm_head.weight":
+                continue
+            shape = self.layout.views[name].shape
+            if name.endswith("c_proj.weight"):
+                t = torch.randn(shape, generator=g) * (cfg.initializer_range / (2 * cfg.n_layer) ** 0.5)
+            elif len(shape) == 2:
+                t = torch.randn(shape, generator=g) * cfg.initializer_range
+            elif name.endswith("ln_1.weight") or name.endswith("ln_2.weight") or "ln_cross_attn.weight" in name \
+                    or name.endswith("ln_f.weight"):
+                t = torch.ones(shape)
+            else:
+                t = torch.zeros(shape)
+            sd[name] = t
+        self.load_state_dict(sd, strict=False)
+
+    def state_dict(self, *args, destination=None, prefix="", keep_vars=False):
+        out = OrderedDict() if destination is None else destination
+        for name in state_dict_names(self.layout):
+            src = "transformer.wte.weight" if name == "lm_head.weight" else name
+            out[prefix + name] = self.view(src).detach()
+        return out
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        names = set(state_dict_names(self.layout))
+        missing = [k for k in names if k not in state_dict and k != "lm_head.weight"]
+        unexpected = [k for k in state_dict if k not in names]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict: missing {missing}, unexpected {unexpected}")
+        for k, v in state_dict.items():
+            if k not in names or k == "lm_head.weight":
+                continue
+            dst = self.view(k)
+            if tuple(v.shape) != tuple(dst.shape):
+                raise RuntimeError(f"size mismatch for {k}: {tuple(v.shape)} vs {tuple(dst.shape)}")
+            dst.copy_(v.to(dst.device, torch.float32))
+        if "lm_head.weight" in state_dict and "transformer.wte.weight" not in state_dict:
+            self.view("transformer.wte.weight").copy_(state_dict["lm_head.weight"])
+        self.refresh_bf16()
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    @torch.no_grad()
+    def refresh_bf16(self) -> None:
+        ops.cast_bf16(self.flat.data, self.flat_b16)
+        self._b16_version = self.flat._version
+
+    def _grad_tmp(self) -> torch.Tensor:
+        if self._tmp is None:
+            self._tmp = torch.zeros_like(self.grad_buf)
+        return self._tmp
+
+    def get_input_embeddings(self):
+        return self.view("transformer.wte.weight")
+
+    def get_output_embeddings(self):
+        return self.view("transformer.wte.weight")
+
+    def num_parameters(self) -> int:
+        """Reference parameter count (tied lm_head counted once, no padding)."""
+        return sum(self.layout.views[k].numel for k in state_dict_names(self.layout) if k != "lm_head.weight")
+
+    # ---- forward ---------------------------------------------------------------------------
+    def _runner(self, B, S, vis_rows, has_feat) -> ModelRunner:
+        key = (B, S, vis_rows, has_feat)
+        r = self._runners.get(key)
+        if r is None:
+            r = ModelRunner(self.layout, self.config, self.flat.data, self.flat_b16, self.grad_buf, B, S, vis_rows,
+                            has_feat, self.process_group)
+            self._runners[key] = r
+        return r
+
+    def forward(self, input_ids=None, past_key_values=None, attention_mask=None, token_type_ids=None,
+                position_ids=None, head_mask=None, inputs_embeds=None, encoder_hidden_states=None,
+                encoder_attention_mask=None, labels=None, emotion_labels=None, use_cache=None,
+                output_attentions=None, output_hidden_states=None, return_dict=None, imgs=None, auds=None,
+                caption_ids=None, visual_feat=None, audio_feat=None):
+        for name, val in (("past_key_values", past_key_values), ("attention_mask", attention_mask),
+                          ("position_ids", position_ids), ("head_mask", head_mask), ("inputs_embeds", inputs_embeds),
+                          ("encoder_hidden_states", encoder_hidden_states),
+                          ("encoder_attention_mask", encoder_attention_mask)):
+            if val is not None:
+                raise NotImplementedError(f"{name} is not supported by the fused training path")
+        if output_attentions or output_hidden_states:
+            raise NotImplementedError("output_attentions / output_hidden_states are not supported")
+        if input_ids is None:
+            raise ValueError("You have to specify either input_ids or inputs_embeds")
+        if caption_ids is None:
+            # src/model.py:521 reads caption_embeds unconditionally: the reference cannot run without it
+            raise ValueError("caption_ids is required (the reference forward reads caption embeddings in every block)")
+        vis = visual_feat if visual_feat is not None else imgs
+        aud = audio_feat if audio_feat is not None else auds
+        if (vis is None) != (aud is None):
+            raise ValueError("imgs/visual_feat and auds/audio_feat must be given together (src/model.py:495-498)")
+        dev = self.flat.device
+        B, S = input_ids.shape
+        E = self.config.n_embd
+
+        def dv(t, dtype):
+            return None if t is None else t.to(dev, dtype, non_blocking=True).contiguous()
+        ids, tt, cap = dv(input_ids, torch.int64), dv(token_type_ids, torch.int64), dv(caption_ids, torch.int64)
+        if tuple(cap.shape) != (B, S):
+            raise ValueError(f"caption_ids must have the text shape {(B, S)} (src/model.py:461), got {tuple(cap.shape)}")
+        if tt is not None and tuple(tt.shape) != (B, S):
+            raise ValueError("token_type_ids must match input_ids")
+        lab = dv(labels, torch.int64)
+        emo_lab = dv(emotion_labels, torch.int64)
+        vis_rows = 0
+        if vis is not None:
+            vis = dv(vis, torch.float32)
+            aud = dv(aud, torch.float32)
+            if vis.dim() == 2:
+                vis = vis.unsqueeze(1)
+            if vis.shape[0] != B or vis.shape[-1] != E or tuple(aud.shape) != (B, E):
+                raise ValueError(f"visual [B,Tv,{E}] / audio [B,{E}] features expected, got {tuple(vis.shape)} / "
+                                 f"{tuple(aud.shape)}")
+            vis_rows = vis.shape[1]
+        if S > self.config.n_positions:
+            raise ValueError(f"sequence length {S} exceeds n_positions {self.config.n_positions}")
+        if self.flat._version != self._b16_version:
+            self.refresh_bf16()  # weights changed outside FusedAdamW (e.g. torch.optim.AdamW)
+        runner = self._runner(B, S, vis_rows, vis is not None)
+        V, Vp = self.config.vocab_size, self.layout.vocab_pad
+        if torch.is_grad_enabled() and self.flat.requires_grad and (lab is not None or emo_lab is not None):
+            loss3, logits, emo = _FusedTrainStep.apply(self.flat, self, runner, ids, tt, cap, vis, aud, lab, emo_lab)
+        else:
+            logits, emo, loss3 = runner.forward(ids, tt, cap, vis, aud, lab, emo_lab, train=False)
+        out = CausalLMOutputWithEmotionClassification(
+            logits=logits.view(B, S, Vp)[:, :, :V], emotion_logits=emo)
+        if loss3 is not None:
+            out.loss = loss3[2] if lab is not None or emo_lab is not None else None
+            out.loss_lm = loss3[0].detach() if lab is not None else None
+            out.loss_emotion = loss3[1].detach() if emo_lab is not None else None
+        return out
+
+
+FusedGPT2LMHead = GPT2LMHeadModel

@@ -1,0 +1,82 @@
+"""FusedAdamW and the polynomial-decay LR schedule of the reference train loop.
+
+``FusedAdamW`` is a ``torch.optim.Optimizer`` with torch.optim.AdamW's hyper-parameters, defaults
+and state_dict format (``exp_avg``, ``exp_avg_sq``, ``step`` per parameter), so
+``get_polynomial_decay_schedule_with_warmup`` (src/main.py:93-95) drives it unchanged and checkpoints
+interchange with ``torch.optim.AdamW`` (src/main.py:68,107).  ``step()`` is one HIP launch over the
+flat parameter buffer (``ergm_adamw_step``) that also refreshes the bf16 weight shadow.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 model=None):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.model = model  # when given, its bf16 shadow is refreshed in the same pass
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise ValueError("FusedAdamW needs contiguous fp32 GPU parameters")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                t = int(st["step"].item())
+                shadow = None
+                if self.model is not None and p is self.model.flat:
+                    shadow = self.model.flat_b16
+                ops.adamw_step(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], shadow, group["lr"], b1, b2,
+                               group["eps"], group["weight_decay"], t)
+                if shadow is not None:
+                    self.model._b16_version = p._version
+        return loss
+
+
+def polynomial_decay_lr_lambda(num_warmup_steps: int, num_training_steps: int, lr_init: float,
+                               lr_end: float = 1e-7, power: float = 2.0):
+    """The LR multiplier of ``get_polynomial_decay_schedule_with_warmup`` (power=2 in the reference,
+    src/main.py:93-95), restated so training does not depend on transformers."""
+    if not lr_init > lr_end:
+        raise ValueError(f"lr_end ({lr_end}) must be smaller than initial lr ({lr_init})")
+
+    def f(step: int) -> float:
+        if step < num_warmup_steps:
+            return float(step) / float(max(1, num_warmup_steps))
+        if step > num_training_steps:
+            return lr_end / lr_init
+        decay_steps = num_training_steps - num_warmup_steps
+        pct_remaining = 1 - (step - num_warmup_steps) / decay_steps
+        return (( lr_init - lr_end) * pct_remaining ** power + lr_end) / lr_init
+    return f
+
+
+def get_polynomial_decay_schedule_with_warmup(optimizer, num_warmup_steps: int, num_training_steps: int,
+                                              lr_end: float = 1e-7, power: float = 1.0, last_epoch: int = -1):
+    lr_init = optimizer.defaults["lr"]
+    return torch.optim.lr_scheduler.LambdaLR(
+        optimizer, polynomial_decay_lr_lambda(num_warmup_steps, num_training_steps, lr_init, lr_end, power), last_epoch)

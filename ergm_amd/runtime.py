@@ -1,0 +1,153 @@
+"""Native runner: binds the flat parameter buffers and a caller-owned workspace to one
+``ergm_model_plan`` (per batch/sequence shape) and drives the C-ABI forward/backward stages.
+
+Data parallelism (one process per GPU, ``torch.distributed`` with backend "nccl" = RCCL over xGMI):
+before the forward the local count of valid LM labels is all-reduced so every rank normalises by the
+GLOBAL count (and the emotion loss by the global batch) — summed gradients then equal the
+single-process gradient of the concatenated global batch.  During backward each
+finished gradient bucket (a contiguous range of the flat gradient buffer) is all-reduced on a side
+stream while later blocks are still being differentiated.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib as L
+from .params import Layout, dp_buckets
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class ModelRunner:
+    def __init__(self, layout: Layout, cfg, flat: torch.Tensor, flat_b16: torch.Tensor, grad: torch.Tensor,
+                 B: int, S: int, vis_rows: int, has_features: bool, process_group=None):
+        self.layout, self.cfg = layout, cfg
+        self.B, self.S = B, S
+        self.dev = flat.device
+        self.lib = L.load()
+        E, Lyr = layout.E, layout.L
+        self.dims = L.ModelDims(vocab=layout.vocab, vocab_pad=layout.vocab_pad, n_embd=E, n_layer=Lyr,
+                                n_head=cfg.n_head, n_inner=layout.F, n_positions=layout.P, batch=B, seq=S,
+                                eps=cfg.layer_norm_epsilon, has_features=int(has_features),
+                                ld_vis=vis_rows * E if has_features else 0)
+        ws_bytes = self.lib.ergm_model_workspace_size(C.byref(self.dims))
+        self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=self.dev)
+        v = layout.views
+        fp, bp, gp = flat.data_ptr(), flat_b16.data_ptr(), grad.data_ptr()
+
+        def f32(name):
+            return C.c_void_p(fp + 4 * v[name].offset)
+
+        def b16(name):
+            return C.c_void_p(bp + 2 * v[name].offset)
+
+        def g32(name):
+            return C.c_void_p(gp + 4 * v[name].offset)
+
+        prm = L.ModelParams()
+        prm.wte, prm.wte_b = f32("__wte_pad"), b16("__wte_pad")
+        prm.wpe = f32("transformer.wpe.weight")
+        prm.ln_f_w, prm.ln_f_b = f32("transformer.ln_f.weight"), f32("transformer.ln_f.bias")
+        prm.emo_w = f32("emotion_head.weight")
+        prm.capkv_w_b, prm.capkv_b = b16("__capkv_w"), f32("__capkv_b")
+        prm.layer_f32 = C.c_void_p(fp + 4 * layout.layer_base[0])
+        prm.layer_b16 = C.c_void_p(bp + 2 * layout.layer_base[0])
+        prm.layer_stride = layout.layer_stride
+        for i, o in enumerate(layout.layer_off):
+            prm.layer_off[i] = o
+        prm.g_wte, prm.g_wpe = g32("__wte_pad"), g32("transformer.wpe.weight")
+        prm.g_ln_f_w, prm.g_ln_f_b = g32("transformer.ln_f.weight"), g32("transformer.ln_f.bias")
+        prm.g_emo_w = g32("emotion_head.weight")
+        prm.g_capkv_w, prm.g_capkv_b = g32("__capkv_w"), g32("__capkv_b")
+        prm.g_layer = C.c_void_p(gp + 4 * layout.layer_base[0])
+        self._params = prm  # keep alive
+        plan = C.c_void_p()
+        L.check(self.lib.ergm_model_create(C.byref(self.dims), C.byref(prm), _p(self.workspace), ws_bytes,
+                                           C.byref(plan)), "ergm_model_create")
+        self.plan = plan
+        self.grad = grad
+        self.pg = process_group
+        self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self.buckets = dp_buckets(layout)
+        self._comm_stream = None
+        self._inputs = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                self.lib.ergm_model_destroy(self.plan)
+        except Exception:
+            pass
+
+    # ---- distributed helpers ------------------------------------------------------------
+    @property
+    def world(self) -> int:
+        if self.pg is None:
+            return 1
+        import torch.distributed as dist
+        return dist.get_world_size(self.pg)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    # ---- forward ------------------------------------------------------------------------
+    def forward(self, ids, tt, cap_ids, vis, aud, labels, emo_labels, train: bool):
+        """Returns (logits [B*S, Vp] bf16, emotion_logits [B, 7] f32, loss3 [3] f32 or None)."""
+        dev, B, S = self.dev, self.B, self.S
+        s = self._stream()
+        if labels is not None:
+            L.check(self.lib.ergm_count_valid(_p(labels), B, S, _p(self.n_valid), s), "ergm_count_valid")
+            if self.world > 1:
+                import torch.distributed as dist
+                dist.all_reduce(self.n_valid[:1], group=self.pg)
+        B_global = B * self.world
+        self._inputs = (ids, tt, cap_ids, vis, aud, labels, emo_labels)  # keep alive through backward
+        L.check(self.lib.ergm_model_set_inputs(self.plan, _p(ids), _p(tt), _p(cap_ids), _p(vis), _p(aud), _p(labels),
+                                               _p(emo_labels), _p(self.n_valid) if labels is not None else None,
+                                               B_global), "ergm_model_set_inputs")
+        logits = torch.empty(B * S, self.layout.vocab_pad, dtype=torch.bfloat16, device=dev)
+        emo = torch.empty(B, 7, dtype=torch.float32, device=dev)
+        loss = torch.empty(3, dtype=torch.float32, device=dev) if (labels is not None or emo_labels is not None) else None
+        L.check(self.lib.ergm_model_forward(self.plan, _p(logits), _p(emo), _p(loss), int(train), s),
+                "ergm_model_forward")
+        return logits, emo, loss
+
+    # ---- backward -----------------------------------------------------------------------
+    def backward(self, grad_scale: Optional[torch.Tensor]) -> None:
+        """Writes every parameter gradient into self.grad (overwrite, not accumulate).  With a
+        process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final."""
+        s = self._stream()
+        lib = self.lib
+        cur = torch.cuda.current_stream(self.dev)
+        works: List = []
+        dp = self.world > 1
+        if dp and self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(self.dev)
+
+        def launch_bucket(k: int):
+            if not dp:
+                return
+            import torch.distributed as dist
+            a, b = self.buckets[k]
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            with torch.cuda.stream(self._comm_stream):
+                self._comm_stream.wait_event(ev)
+                works.append(dist.all_reduce(self.grad[a:b], group=self.pg, async_op=True))
+
+        L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
+        Lyr = self.layout.L
+        for i, l in enumerate(reversed(range(Lyr))):
+            L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
+            launch_bucket(i)
+        L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
+        launch_bucket(Lyr)
+        for w in works:
+            w.wait()  # makes the current stream wait for the collective (no host sync)
+        if dp:
+            cur.wait_stream(self._comm_stream)
