@@ -75,6 +75,7 @@ _SIGS = {
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),
+    "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
     "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
     "ergm_model_forward": (i32, [vp, vp, vp, vp, i32, vp]),
     "ergm_model_backward_head": (i32, [vp, vp, vp]),

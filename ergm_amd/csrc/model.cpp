@@ -53,6 +53,9 @@ struct ergm_model_plan {
     const int* n_valid;
     int B_global;
     bool have_fwd;
+    // kernel probe (bench timing)
+    int probe;
+    hipEvent_t ev_begin, ev_end;
     // dry-run sizing
     bool dry;
     size_t need;
@@ -150,6 +153,18 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
                               T, E, s);
 }
 
+struct Probe {  // records the probe events around one launch when `id` is the active probe
+    ergm_model_plan* P;
+    bool on;
+    hipStream_t s;
+    Probe(ergm_model_plan* P_, int id, hipStream_t s_) : P(P_), on(!P_->dry && P_->probe == id && P_->ev_begin), s(s_) {
+        if (on) hipEventRecord(P->ev_begin, s);
+    }
+    ~Probe() {
+        if (on) hipEventRecord(P->ev_end, s);
+    }
+};
+
 inline const float* LF(const ergm_model_plan* P, int l, int t) {
     return P->p.layer_f32 + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
 }
@@ -217,12 +232,23 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->vis = P->aud = nullptr;
     P->n_valid = nullptr;
     P->B_global = d.batch;
+    P->probe = 0;
+    P->ev_begin = P->ev_end = nullptr;
     *out = P;
     return ERGM_OK;
 }
 
 extern "C" int ergm_model_destroy(ergm_model_plan* P) {
     delete P;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begin, void* ev_end) {
+    ERGM_CHECK_ARG(P && probe >= 0 && probe <= 4, "model_set_probe: bad probe");
+    ERGM_CHECK_ARG(probe == 0 || (ev_begin && ev_end), "model_set_probe: events required");
+    P->probe = probe;
+    P->ev_begin = reinterpret_cast<hipEvent_t>(ev_begin);
+    P->ev_end = reinterpret_cast<hipEvent_t>(ev_end);
     return ERGM_OK;
 }
 
@@ -251,8 +277,11 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         ERGM_TRY(ergm_embed_fwd(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap, B,
                             S, E, d.vocab, s));
     // all L cross-attention K/V projections of the caption embeddings in one GEMM
+    {
+    Probe pr(P, 4, s);
     ERGM_TRY(gemm(P, s, T, L2E, E, P->cap, E, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
                   ERGM_EPI_BIAS, p.capkv_b));
+    }
     for (int l = 0; l < L; ++l) {
         LayerActs& a = P->la[l];
         float* x0 = P->resid[3 * l];
@@ -289,8 +318,11 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     if (!P->dry)
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
-    ERGM_TRY(gemm(P, s, T, d.vocab_pad, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad, ERGM_BF16,
-                  ERGM_EPI_NONE));
+    {
+        Probe pr(P, 1, s);
+        ERGM_TRY(gemm(P, s, T, d.vocab_pad, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
+                      ERGM_BF16, ERGM_EPI_NONE));
+    }
     if (P->dry) return ERGM_OK;
     ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, B, S, E, 7,
                                P->B_global, nullptr, s));
@@ -327,10 +359,16 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad;
     // dh_f = dlogits · wte  (contraction over the padded vocab), dwte = dlogitsᵀ · ln_f(h)
-    ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
-                  nullptr, nullptr, 0, nullptr, 0, gscale));
-    ERGM_TRY(gemm(P, s, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32, ERGM_EPI_NONE,
-                  nullptr, nullptr, 0, nullptr, 0, gscale));
+    {
+        Probe pr(P, 2, s);
+        ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
+                      nullptr, nullptr, 0, nullptr, 0, gscale));
+    }
+    {
+        Probe pr(P, 3, s);
+        ERGM_TRY(gemm(P, s, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
+                      ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, gscale));
+    }
     if (P->dry) return ERGM_OK;
     if (P->emo_labels) {
         ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w, P->dy, B,

@@ -232,6 +232,12 @@ int ergm_model_backward_head(ergm_model_plan* plan, const float* grad_scale_dev,
 int ergm_model_backward_layer(ergm_model_plan* plan, int layer, void* stream);
 int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
 
+/* Kernel probe for in-loop timing: while set, the executor records `ev_begin` / `ev_end`
+ * (hipEvent_t, passed as void*) on the stream immediately around the probed launch:
+ *   1 = tied LM-head forward GEMM      2 = LM-head dX GEMM      3 = LM-head dW GEMM
+ *   4 = stacked caption-K/V forward GEMM (all blocks)        0 = off                         */
+int ergm_model_set_probe(ergm_model_plan* plan, int probe, void* ev_begin, void* ev_end);
+
 /* Library information and errors. */
 int ergm_version(void);
 int ergm_last_error(char* buf, size_t n);
