@@ -1,0 +1,206 @@
+"""Benchmark: utterances/s of the full ERGM training step (forward + backward + AdamW + LR step) on
+MELD-shaped synthetic batches, GPT-2-small + audio/visual fusion, batch 16 per GPU, bf16 MFMA
+(BASELINE.json configs[1]; with --gpus N one process per GPU over RCCL, configs[2]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0.  ``value`` = all utterances processed by all ranks ÷ the max over
+ranks of the wall time of exactly K steps (barrier + device sync on both sides).  ``roofline`` is
+for the tied LM-head forward GEMM (the single largest GEMM launch of the step, a kernel symbol that
+nothing else in the step uses), timed with HIP events recorded by the native executor around that
+launch inside the timed steps; ``mfma_step`` is the whole step's algorithmic FLOPs
+over the step time against the 2.5 PF/s dense bf16 peak.  ``cpu_baseline`` times the CPU oracle
+(fp32 PyTorch restatement of the reference step) on the host cores for a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+CONFIGS = {
+    # name: (S, turns, batch per GPU, description)
+    "c2": (128, 5, 16, "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
+    "c4": (512, 20, 8, "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
+}
+
+
+def flops_per_utterance(S: int, E: int = 768, L: int = 12, V: int = 50260) -> float:
+    """3·S·[L·(28E² + 4E²·Sc/S + 2SE + 4ScE) + 2EV] with Sc = S (causal self-attention
+    counted at S²/2, cross-attention in full; LN/softmax/CE/AdamW/embedding excluded)."""
+    Sc = S
+    f_tok = L * (28 * E * E + 4 * E * E * Sc / S + 2 * S * E + 4 * Sc * E) + 2 * E * V
+    return 3.0 * S * f_tok
+
+
+def cpu_baseline(S, turns, B, seconds_target=20.0):
+    """Time the CPU oracle (fp32) doing the same train step on a bounded sample."""
+    from oracle import gpt2_oracle as O
+    from ergm_amd.data import synthetic_batch
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(n)
+    cfg = O.OracleConfig()
+    P = O.init_params(cfg, seed=0, perturb=False)
+    st = O.AdamWState()
+    batch = synthetic_batch(B, S, n_turns=turns, seed=123)
+    lr = 2e-5
+    _, g = O.loss_and_grads(P, cfg, batch)  # warm-up step
+    O.adamw_step(P, g, st, lr)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        _, g = O.loss_and_grads(P, cfg, batch)
+        O.adamw_step(P, g, st, lr)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_target or steps >= 3:
+            break
+    return {"value": round(B * steps / el, 4), "unit": "utterances/s", "cores": n, "kind": "port",
+            "sample": f"{steps} full fp32 train steps (fwd+bwd+AdamW) of the CPU oracle at B={B}, S={S}, "
+                      f"GPT-2-small+fusion, after 1 warm-up step; torch CPU threads={n}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from ergm_amd import _lib
+    from ergm_amd.config import gpt2_small
+    from ergm_amd.data import synthetic_batch
+    from ergm_amd.model import GPT2LMHeadModel
+    from ergm_amd.optim import FusedAdamW, get_polynomial_decay_schedule_with_warmup
+
+    S, turns, B, desc = CONFIGS[args.config]
+    cfg = gpt2_small()
+    model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
+    model.init_weights(seed=0)
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model)
+    total = args.warmup + args.steps
+    sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=int(0.1 * total),
+                                                      num_training_steps=total, power=2)
+    batch = synthetic_batch(B, S, n_turns=turns, seed=1000 + rank)
+    kw = dict(input_ids=batch["input_ids"], token_type_ids=batch["token_type_ids"], labels=batch["labels"],
+              emotion_labels=batch["emotion_labels"], caption_ids=batch["caption_ids"], imgs=batch["visual_feat"],
+              auds=batch["audio_feat"])
+    kw = {k: v.to(dev) for k, v in kw.items()}  # inputs resident in HBM before timing
+    loss_acc = torch.zeros(2, device=dev)
+    correct = torch.zeros(1, device=dev, dtype=torch.int64)
+
+    def step():
+        out = model(**kw)
+        opt.zero_grad()
+        out.loss.backward()
+        opt.step()
+        sched.step()
+        # the trainer's per-step metrics (src/main.py:158-169), kept on device (no host sync)
+        loss_acc[0] += out.loss.detach()
+        loss_acc[1] += out.loss_lm
+        correct.add_((out.emotion_logits.argmax(-1) == kw["emotion_labels"]).sum())
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    runner = next(iter(model._runners.values()))
+    lib = _lib.load()
+    import ctypes as C
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        e0, e1 = evs[i]
+        lib.ergm_model_set_probe(runner.plan, args.probe, C.c_void_p(e0.cuda_event), C.c_void_p(e1.cuda_event))
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lib.ergm_model_set_probe(runner.plan, 0, None, None)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    probe_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    utt = B * world * args.steps
+    value = utt / dt
+    ms_step = 1000.0 * dt / args.steps
+    T = B * S
+    V, E = cfg.vocab_size, cfg.n_embd
+    probe_flops = {1: 2.0 * T * V * E, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
+                   4: 2.0 * T * E * (2 * E * cfg.n_layer)}[args.probe]
+    probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (gemm_kernel<128,128,MK,NK,none,bf16>)",
+                  2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
+    achieved = probe_flops / (probe_ms * 1e-3) / 1e12
+    step_flops = flops_per_utterance(S) * B
+    rec = {
+        "metric": "utterances/sec training, MELD-shape synthetic batch, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "utterances/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded MELD-shape token/feature batches; random-init GPT-2-small weights)",
+        "config": {"workload": desc, "model": "GPT-2-small (L=12, E=768, H=12, V=50260) + cross-attention "
+                   "caption fusion + emotion head", "global_batch": B * world, "seq_len": S,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": round(achieved, 1),
+                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": None, "avg_launch_ms": round(probe_ms, 4),
+                     "flops_per_launch": probe_flops},
+        "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
+                      "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                      "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S), 0)},
+        "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
+                          "emotion_acc": round(correct.item() / (B * total), 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(S, turns, B)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
