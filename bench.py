@@ -131,7 +131,7 @@ def main():
     runner = next(iter(model._runners.values()))
     lib = _lib.load()
     import ctypes as C
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(_lib.HipEvent(), _lib.HipEvent()) for _ in range(args.steps)]
 
     def barrier():
         if world > 1:
@@ -143,7 +143,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         e0, e1 = evs[i]
-        lib.ergm_model_set_probe(runner.plan, args.probe, C.c_void_p(e0.cuda_event), C.c_void_p(e1.cuda_event))
+        _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
         step()
     torch.cuda.synchronize()
     barrier()
@@ -155,7 +155,7 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    probe_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    probe_ms = sum(a.elapsed_ms(b) for a, b in evs) / len(evs)
     utt = B * world * args.steps
     value = utt / dt
     ms_step = 1000.0 * dt / args.steps

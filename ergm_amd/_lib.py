@@ -127,5 +127,39 @@ def check(rc: int, what: str) -> None:
     raise ErgmError(msg)
 
 
+class HipEvent:
+    """A raw hipEvent_t (libamdhip64) for in-loop kernel timing by the native executor's probe."""
+    _hip = None
+
+    def __init__(self):
+        if HipEvent._hip is None:
+            h = C.CDLL("libamdhip64.so")
+            h.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+            h.hipEventDestroy.argtypes = [C.c_void_p]
+            h.hipEventSynchronize.argtypes = [C.c_void_p]
+            h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+            HipEvent._hip = h
+        self.ev = C.c_void_p()
+        if HipEvent._hip.hipEventCreate(C.byref(self.ev)) != 0:
+            raise ErgmError("hipEventCreate failed")
+
+    def elapsed_ms(self, end: "HipEvent") -> float:
+        h = HipEvent._hip
+        if h.hipEventSynchronize(end.ev) != 0:
+            raise ErgmError("hipEventSynchronize failed")
+        ms = C.c_float()
+        rc = h.hipEventElapsedTime(C.byref(ms), self.ev, end.ev)
+        if rc != 0:
+            raise ErgmError(f"hipEventElapsedTime failed ({rc})")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.ev and HipEvent._hip is not None:
+                HipEvent._hip.hipEventDestroy(self.ev)
+        except Exception:
+            pass
+
+
 def call(name: str, *args) -> None:
     check(getattr(load(), name)(*args), name)

@@ -1,0 +1,79 @@
+"""Data-parallel synchronisation for the fused training step (one process per GPU).
+
+The reference trains on one device (src/main.py:40-43) and has no collective; the build adds pure
+data parallelism:
+
+1. Loss normalisation.  The reference LM loss is a mean over the valid (!= -100) shifted labels of the
+   whole batch and the emotion loss a mean over the batch (src/model.py:704-713).  Each rank therefore
+   divides its local sums by the GLOBAL valid-label count (all-reduced before the forward) and by the
+   global batch, so the SUM over ranks of local gradients equals the gradient of the concatenated
+   global batch on one device.
+2. Gradient all-reduce (SUM) of contiguous buckets of the flat gradient buffer, launched on a side
+   stream as soon as the backward stage that finalises each bucket has been enqueued, so RCCL over
+   xGMI overlaps the remaining backward.  The last bucket (caption K/V + wpe + wte) is final only after
+   the embedding backward and cannot overlap.
+
+Works with any torch.distributed backend: "nccl" (= RCCL on ROCm) on GPUs, "gloo" for CPU tests.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+
+class DPSync:
+    def __init__(self, process_group=None, buckets: Optional[List[Tuple[int, int]]] = None):
+        self.pg = process_group
+        self.buckets = buckets or []
+        self._works: List = []
+        self._stream = None
+
+    @property
+    def world(self) -> int:
+        if self.pg is None:
+            return 1
+        import torch.distributed as dist
+        return dist.get_world_size(self.pg)
+
+    @property
+    def active(self) -> bool:
+        return self.world > 1
+
+    def reduce_count(self, n_valid: torch.Tensor) -> None:
+        """In place: local valid-label count -> global count (before the forward)."""
+        if self.active:
+            import torch.distributed as dist
+            dist.all_reduce(n_valid, group=self.pg)
+
+    def global_batch(self, local_batch: int) -> int:
+        return local_batch * self.world
+
+    def begin(self) -> None:
+        self._works = []
+
+    def bucket_ready(self, k: int, grad: torch.Tensor) -> None:
+        """Start the all-reduce of bucket k of the flat gradient buffer `grad`."""
+        if not self.active:
+            return
+        import torch.distributed as dist
+        a, b = self.buckets[k]
+        if grad.is_cuda:
+            cur = torch.cuda.current_stream(grad.device)
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(grad.device)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            with torch.cuda.stream(self._stream):
+                self._stream.wait_event(ev)
+                self._works.append(dist.all_reduce(grad[a:b], group=self.pg, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(grad[a:b], group=self.pg, async_op=True))
+
+    def finish(self, grad: torch.Tensor) -> None:
+        """Make the current stream wait for every outstanding bucket (no host synchronisation)."""
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if grad.is_cuda and self._stream is not None:
+            torch.cuda.current_stream(grad.device).wait_stream(self._stream)

@@ -11,11 +11,12 @@ stream while later blocks are still being differentiated.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, List, Optional, Tuple
+from typing import Optional
 
 import torch
 
 from . import _lib as L
+from .dist import DPSync
 from .params import Layout, dp_buckets
 
 
@@ -71,10 +72,8 @@ class ModelRunner:
                                            C.byref(plan)), "ergm_model_create")
         self.plan = plan
         self.grad = grad
-        self.pg = process_group
+        self.dp = DPSync(process_group, dp_buckets(layout))
         self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)
-        self.buckets = dp_buckets(layout)
-        self._comm_stream = None
         self._inputs = None
 
     def __del__(self):
@@ -83,14 +82,6 @@ class ModelRunner:
                 self.lib.ergm_model_destroy(self.plan)
         except Exception:
             pass
-
-    # ---- distributed helpers ------------------------------------------------------------
-    @property
-    def world(self) -> int:
-        if self.pg is None:
-            return 1
-        import torch.distributed as dist
-        return dist.get_world_size(self.pg)
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
@@ -102,10 +93,8 @@ class ModelRunner:
         s = self._stream()
         if labels is not None:
             L.check(self.lib.ergm_count_valid(_p(labels), B, S, _p(self.n_valid), s), "ergm_count_valid")
-            if self.world > 1:
-                import torch.distributed as dist
-                dist.all_reduce(self.n_valid[:1], group=self.pg)
-        B_global = B * self.world
+            self.dp.reduce_count(self.n_valid[:1])
+        B_global = self.dp.global_batch(B)
         self._inputs = (ids, tt, cap_ids, vis, aud, labels, emo_labels)  # keep alive through backward
         L.check(self.lib.ergm_model_set_inputs(self.plan, _p(ids), _p(tt), _p(cap_ids), _p(vis), _p(aud), _p(labels),
                                                _p(emo_labels), _p(self.n_valid) if labels is not None else None,
@@ -123,31 +112,12 @@ class ModelRunner:
         process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final."""
         s = self._stream()
         lib = self.lib
-        cur = torch.cuda.current_stream(self.dev)
-        works: List = []
-        dp = self.world > 1
-        if dp and self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(self.dev)
-
-        def launch_bucket(k: int):
-            if not dp:
-                return
-            import torch.distributed as dist
-            a, b = self.buckets[k]
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            with torch.cuda.stream(self._comm_stream):
-                self._comm_stream.wait_event(ev)
-                works.append(dist.all_reduce(self.grad[a:b], group=self.pg, async_op=True))
-
+        self.dp.begin()
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
         Lyr = self.layout.L
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
-            launch_bucket(i)
+            self.dp.bucket_ready(i, self.grad)
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
-        launch_bucket(Lyr)
-        for w in works:
-            w.wait()  # makes the current stream wait for the collective (no host sync)
-        if dp:
-            cur.wait_stream(self._comm_stream)
+        self.dp.bucket_ready(Lyr, self.grad)
+        self.dp.finish(self.grad)

@@ -1,0 +1,97 @@
+"""Data-parallel logic on CPU (gloo, world_size 2): per-rank gradients normalised by the GLOBAL label
+count / batch, laid into the flat gradient buffer and all-reduced bucket by bucket by
+``ergm_amd.dist.DPSync``, must equal the single-process gradient of the concatenated batch.
+The per-rank gradients come from the CPU oracle (the checker); what is under test is the product's
+normalisation contract, flat layout and bucket schedule."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ergm_amd.data import synthetic_batch
+from ergm_amd.dist import DPSync
+from ergm_amd.params import build_layout, dp_buckets
+from oracle import gpt2_oracle as O
+
+CFG = O.OracleConfig(vocab_size=256, n_embd=64, n_layer=3, n_head=1, n_positions=64)
+B, S = 4, 32
+
+
+def _batch():
+    b = synthetic_batch(B, S, n_turns=3, feat_dim=CFG.n_embd, seed=9, vocab_hi=250, sp1=254, sp2=255, eos=249)
+    b["labels"][1, :] = -100            # uneven valid-label counts across ranks
+    b["labels"][1, -3:] = b["input_ids"][1, -3:]
+    return b
+
+
+def _flat_grads(layout, grads):
+    g = torch.zeros(layout.total)
+    for k, v in grads.items():
+        view = layout.views[k]
+        g.as_strided(view.shape, view.stride, view.offset).copy_(v)
+    return g
+
+
+def _worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    P = O.init_params(CFG, seed=4)
+    full = _batch()
+    lo, hi = rank * B // world, (rank + 1) * B // world
+    local = {k: v[lo:hi].clone() for k, v in full.items()}
+    layout = build_layout(CFG.vocab_size, CFG.n_embd, CFG.n_layer, CFG.inner, CFG.n_positions)
+    dp = DPSync(dist.group.WORLD, dp_buckets(layout))
+    n = (local["labels"][:, 1:] != -100).sum().reshape(1).to(torch.int32)
+    n_local = int(n.item())
+    dp.reduce_count(n)
+    n_global = int(n.item())
+    leaves = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    out = O.forward(leaves, CFG, **local)
+    loss = out["loss_lm"] * (n_local / n_global) + out["loss_emotion"] * ((hi - lo) / dp.global_batch(hi - lo))
+    loss.backward()
+    grad = _flat_grads(layout, {k: v.grad for k, v in leaves.items()})
+    dp.begin()
+    for k in range(len(dp.buckets)):
+        dp.bucket_ready(k, grad)
+    dp.finish(grad)
+    if rank == 0:
+        torch.save(grad, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_buckets_partition_the_flat_buffer():
+    layout = build_layout(50260, 768, 12, 3072, 1024)
+    b = dp_buckets(layout)
+    assert b[0][0] == 0 and b[-1][1] == layout.total
+    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    assert len(b) == 13  # (head + block 11), blocks 10..0, embeddings
+    # every named tensor lies inside exactly one bucket
+    for name, v in layout.views.items():
+        last = v.offset + sum((s - 1) * st for s, st in zip(v.shape, v.stride))
+        inside = [i for i, (a, e) in enumerate(b) if a <= v.offset and last < e]
+        assert len(inside) == 1, name
+
+
+def test_dp2_matches_single_process_gradient():
+    path = os.path.join(tempfile.mkdtemp(), "g.pt")
+    mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    got = torch.load(path, weights_only=True)
+    P = O.init_params(CFG, seed=4)
+    _, ref = O.loss_and_grads(P, CFG, _batch())
+    layout = build_layout(CFG.vocab_size, CFG.n_embd, CFG.n_layer, CFG.inner, CFG.n_positions)
+    want = _flat_grads(layout, ref)
+    err = ((got - want).norm() / want.norm()).item()
+    assert err < 1e-5, err
