@@ -67,7 +67,7 @@ _SIGS = {
     "ergm_embed_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, vp]),
     "ergm_count_valid": (i32, [vp, i32, i32, vp, vp]),
     "ergm_xent_fwd_bwd": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
-    "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
+    "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ergm_loss_finalize": (i32, [vp, i32, vp, vp, i32, vp, vp]),
     "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, vp]),
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),

@@ -16,8 +16,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const int64_t* __restrict__ cap_ids, const float* __restrict__ wte,
                                                         const float* __restrict__ wpe, const float* __restrict__ vis,
                                                         int ld_vis, const float* __restrict__ aud,
-                                                        float* __restrict__ h0, __bf16* __restrict__ cap, int B, int S,
-                                                        int E, int V) {
+                                                        float* __restrict__ h0, __bf16* __restrict__ cap, int ld_cap,
+                                                        int B, int S, int E, int V) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + wave;
     if (t >= B * S) return;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
         float4 cv = ok_c ? *reinterpret_cast<const float4*>(wte + (size_t)cid * E + c) : make_float4(0, 0, 0, 0);
         bf16x4 cb;
         cb[0] = f2bf(cv.x); cb[1] = f2bf(cv.y); cb[2] = f2bf(cv.z); cb[3] = f2bf(cv.w);
-        *reinterpret_cast<bf16x4*>(cap + (size_t)t * E + c) = cb;
+        *reinterpret_cast<bf16x4*>(cap + (size_t)t * ld_cap + c) = cb;
     }
 }
 
@@ -89,11 +89,60 @@ __global__ __launch_bounds__(1024) void embed_sort_kernel(const int64_t* __restr
     for (int i = threadIdx.x; i < n; i += 1024) out[i] = key[i];
 }
 
-// One workgroup per sorted position; only segment heads work: dwte[id] += Σ rows of the segment.
+// Pass 1: one workgroup per chunk of SEG_CH sorted positions.  Every maximal run of equal ids inside
+// the chunk is summed in position order and written to part[run start].
+constexpr int SEG_CH = 64;
+
+__device__ __forceinline__ const float* seg_row(uint64_t key, int T, const float* dh0, const float* dcap, int E) {
+    int e = (int)(uint32_t)key;
+    return e < 2 * T ? dh0 + (size_t)(e < T ? e : e - T) * E : dcap + (size_t)(e - 2 * T) * E;
+}
+
 template <int NC>
-__global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __restrict__ keys, int n, int T,
+__global__ __launch_bounds__(256) void embed_runsum_kernel(const uint64_t* __restrict__ keys, int n, int T,
                                                            const float* __restrict__ dh0, const float* __restrict__ dcap,
-                                                           float* __restrict__ dwte, int E) {
+                                                           float* __restrict__ part, int E) {
+    const int p0 = blockIdx.x * SEG_CH, p1 = min(n, p0 + SEG_CH);
+    float acc[NC];
+    int start = p0;
+    uint32_t id = (uint32_t)(keys[p0] >> 32);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+    for (int q = p0; q < p1; ++q) {
+        const uint64_t kq = keys[q];
+        if (kq == ~0ull) break;
+        const uint32_t iq = (uint32_t)(kq >> 32);
+        if (iq != id) {
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                int c = threadIdx.x + j * 256;
+                if (c < E) part[(size_t)start * E + c] = acc[j];
+                acc[j] = 0.f;
+            }
+            start = q;
+            id = iq;
+        }
+        const float* row = seg_row(kq, T, dh0, dcap, E);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            int c = threadIdx.x + j * 256;
+            if (c < E) acc[j] += row[c];
+        }
+    }
+    if (keys[p0] == ~0ull) return;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        int c = threadIdx.x + j * 256;
+        if (c < E) part[(size_t)start * E + c] = acc[j];
+    }
+}
+
+// Pass 2: one workgroup per sorted position; segment heads add their run partials (the run at the
+// head, then one run per following chunk while the id continues) in order to dwte[id].
+template <int NC>
+__global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __restrict__ keys, int n,
+                                                           const float* __restrict__ part, float* __restrict__ dwte,
+                                                           int E) {
     const int p = blockIdx.x;
     const uint64_t k = keys[p];
     if (k == ~0ull) return;
@@ -101,16 +150,17 @@ __global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __res
     if (p > 0 && (uint32_t)(keys[p - 1] >> 32) == id) return;
     float acc[NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
-    for (int q = p; q < n; ++q) {
+    for (int j = 0; j < NC; ++j) {
+        int c = threadIdx.x + j * 256;
+        acc[j] = c < E ? part[(size_t)p * E + c] : 0.f;
+    }
+    for (int q = (p / SEG_CH + 1) * SEG_CH; q < n; q += SEG_CH) {
         uint64_t kq = keys[q];
         if (kq == ~0ull || (uint32_t)(kq >> 32) != id) break;
-        int e = (int)(uint32_t)kq;
-        const float* row = e < 2 * T ? dh0 + (size_t)(e < T ? e : e - T) * E : dcap + (size_t)(e - 2 * T) * E;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             int c = threadIdx.x + j * 256;
-            if (c < E) acc[j] += row[c];
+            if (c < E) acc[j] += part[(size_t)q * E + c];
         }
     }
     float* dst = dwte + (size_t)id * E;
@@ -135,28 +185,39 @@ static int next_pow2(int x) {
 
 using namespace ergm;
 
-extern "C" int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
-                              const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0, void* cap,
-                              int B, int S, int E, int V, void* stream) {
+namespace ergm {
+int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
+                 const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
+                 int V, hipStream_t s) {
     ERGM_CHECK_ARG(ids && cap_ids && wte && wpe && h0 && cap, "embed_fwd: null argument");
     ERGM_CHECK_ARG(B > 0 && S > 0 && E > 0 && E % 4 == 0 && E <= 1024 && V > 0, "embed_fwd: bad shape");
     ERGM_CHECK_ARG((vis == nullptr) == (aud == nullptr), "embed_fwd: visual and audio features go together");
     ERGM_CHECK_ARG(!vis || (ld_vis >= E && ld_vis % 4 == 0), "embed_fwd: bad ld_vis");
     const int T = B * S;
     dim3 grid(cdiv(T, 4));
-    hipStream_t s = as_stream(stream);
+    ERGM_CHECK_ARG(ld_cap >= E && ld_cap % 4 == 0, "embed_fwd: bad ld_cap");
     auto* cb = reinterpret_cast<__bf16*>(cap);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, B, S, E, V); break;
-        case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, B, S, E, V); break;
-        case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, B, S, E, V); break;
-        default: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, B, S, E, V); break;
+        case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
+        case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
+        case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
+        default: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
     }
     return check_launch("embed_fwd");
 }
+}  // namespace ergm
+
+extern "C" int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
+                              const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0, void* cap,
+                              int B, int S, int E, int V, void* stream) {
+    return embed_fwd_ld(ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cap, E, B, S, E, V, as_stream(stream));
+}
+
+static size_t keys_bytes(int T) { return ((size_t)3 * T * sizeof(uint64_t) + 255) & ~(size_t)255; }
 
 extern "C" size_t ergm_embed_bwd_workspace_size(int T) {
-    return (size_t)3 * T * sizeof(uint64_t) + 256;
+    // sorted keys + one partial row per sorted position (run sums); E <= 1024
+    return keys_bytes(T) + (size_t)3 * T * 1024 * sizeof(float);
 }
 
 extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* dh0,
@@ -180,12 +241,19 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
     }
     hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), (size_t)npad * sizeof(uint64_t), s, ids, tt, cap_ids, T,
                        V, npad, keys);
+    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + keys_bytes(T));
+    const int n = 3 * T;
+    dim3 g1(cdiv(n, SEG_CH)), g2(n);
+#define ERGM_SEG(NC)                                                                                         \
+    hipLaunchKernelGGL(embed_runsum_kernel<NC>, g1, dim3(256), 0, s, keys, n, T, dh0, dcap, part, E);         \
+    hipLaunchKernelGGL(embed_segsum_kernel<NC>, g2, dim3(256), 0, s, keys, n, part, dwte, E);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(embed_segsum_kernel<1>, dim3(3 * T), dim3(256), 0, s, keys, 3 * T, T, dh0, dcap, dwte, E); break;
-        case 2: hipLaunchKernelGGL(embed_segsum_kernel<2>, dim3(3 * T), dim3(256), 0, s, keys, 3 * T, T, dh0, dcap, dwte, E); break;
-        case 3: hipLaunchKernelGGL(embed_segsum_kernel<3>, dim3(3 * T), dim3(256), 0, s, keys, 3 * T, T, dh0, dcap, dwte, E); break;
-        default: hipLaunchKernelGGL(embed_segsum_kernel<4>, dim3(3 * T), dim3(256), 0, s, keys, 3 * T, T, dh0, dcap, dwte, E); break;
+        case 1: ERGM_SEG(1) break;
+        case 2: ERGM_SEG(2) break;
+        case 3: ERGM_SEG(3) break;
+        default: ERGM_SEG(4) break;
     }
+#undef ERGM_SEG
     ERGM_TRY(check_launch("embed_bwd"));
     // dwpe[s][e] = Σ_b dh0[b][s][e]   (rows b of [B][S*E])
     return colsum_impl(dh0, false, B, S * E, S * E, dwpe, 0, nullptr, 0, s);

@@ -11,6 +11,8 @@
 // k-contiguous tiles are read row-wise with ds_read_b128 (16-B chunk XOR row&7 swizzle);
 // m/n-contiguous tiles are read column-wise with ds_read_b64_tr_b16 (CDNA4 transpose read) under a
 // row-dependent chunk XOR that keeps each 32-lane half conflict-free.
+#include <algorithm>
+
 #include "common.h"
 
 namespace ergm {
@@ -262,22 +264,27 @@ struct GemmPlan {
 };
 
 static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
+    // Tile / split-K choice: fill the 256 CUs with >= ~200 workgroups; very deep K (LM-head dX over
+    // the vocabulary, the stacked caption K/V dX) goes to 128x128 tiles split along K.
     GemmPlan p;
     const int M = d->M, N = d->N, K = d->K;
-    long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
-    long t64 = (long)cdiv(M, 64) * cdiv(N, 64);
-    bool can128 = !(d->a_layout == ERGM_KM && M % 8) && !(d->b_layout == ERGM_KN && N % 8);
-    if (can128 && t128 >= 240) { p.bm = 128; p.bn = 128; }
-    else { p.bm = 64; p.bn = 64; }
-    long tiles = (long)cdiv(M, p.bm) * cdiv(N, p.bn);
+    const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
+    const long t64 = (long)cdiv(M, 64) * cdiv(N, 64);
     int split = 1;
-    if (d->split_k > 1) split = d->split_k;
-    else if (d->split_k == 0 && tiles < 200 && K >= 1024) {
-        split = (int)((400 + tiles - 1) / tiles);
-        int maxs = K / 512;
-        if (split > maxs) split = maxs;
-        if (split < 1) split = 1;
+    if (t128 >= 240) {
+        p.bm = p.bn = 128;
+    } else if (K >= 4096 && d->split_k != 1) {
+        p.bm = p.bn = 128;
+        split = (int)((512 + t128 - 1) / t128);
+        split = std::max(1, std::min(split, K / 1024));
+    } else {
+        p.bm = p.bn = 64;
+        if (t64 < 200 && K >= 1024 && d->split_k != 1) {
+            split = (int)((400 + t64 - 1) / t64);
+            split = std::max(1, std::min(split, K / 512));
+        }
     }
+    if (d->split_k > 1) split = d->split_k;
     int kps = cdiv(cdiv(K, split), GEMM_BK) * GEMM_BK;
     split = cdiv(K, kps);
     p.split = split;
@@ -338,8 +345,9 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     ERGM_CHECK_ARG(d->b_layout == ERGM_NK || d->b_layout == ERGM_KN, "ergm_gemm: bad b_layout");
     ERGM_CHECK_ARG(d->a_layout == ERGM_MK ? d->lda >= d->K : d->lda >= d->M, "ergm_gemm: lda too small");
     ERGM_CHECK_ARG(d->b_layout == ERGM_NK ? d->ldb >= d->K : d->ldb >= d->N, "ergm_gemm: ldb too small");
-    ERGM_CHECK_ARG(d->a_layout == ERGM_MK || d->M % 8 == 0, "ergm_gemm: KM layout needs M %% 8 == 0");
-    ERGM_CHECK_ARG(d->b_layout == ERGM_NK || d->N % 8 == 0, "ergm_gemm: KN layout needs N %% 8 == 0");
+    // m/n-contiguous operands are staged in whole 16-B chunks: the row must hold round_up(M|N, 8)
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK || d->lda >= ((d->M + 7) & ~7), "ergm_gemm: KM layout needs lda >= round8(M)");
+    ERGM_CHECK_ARG(d->b_layout == ERGM_NK || d->ldb >= ((d->N + 7) & ~7), "ergm_gemm: KN layout needs ldb >= round8(N)");
     ERGM_CHECK_ARG(d->ldc >= d->N, "ergm_gemm: ldc < N");
     ERGM_CHECK_ARG(d->c_dtype == ERGM_F32 || d->c_dtype == ERGM_BF16, "ergm_gemm: bad c_dtype");
     int e = d->epilogue;

@@ -22,6 +22,15 @@
 
 using namespace ergm;
 
+namespace ergm {
+int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
+                     int rows, int E, float eps, hipStream_t s);
+int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
+int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
+                 const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
+                 int V, hipStream_t s);
+}  // namespace ergm
+
 struct LayerActs {
     __bf16 *ln1, *lnx, *ln2;
     float *m1, *r1, *mx, *rx, *m2, *r2;
@@ -33,6 +42,10 @@ struct ergm_model_plan {
     ergm_model_dims d;
     ergm_model_params p;
     int T, L2E;
+    // Activations that feed a weight-gradient GEMM carry a constant ones column (index E or F) so the
+    // dW GEMM over K+1 rows also yields the bias gradient (each bias is stored right after its weight).
+    int XE, XF;
+    bool fused_bias;
     // activations
     float** resid;  // 3L+1 residual-stream tensors [T][E] f32
     std::vector<float*> resid_v;
@@ -80,28 +93,31 @@ size_t carve(ergm_model_plan* P, char* base) {
     const ergm_model_dims& d = P->d;
     const size_t T = (size_t)d.batch * d.seq, E = d.n_embd, F = d.n_inner, L = d.n_layer;
     const size_t BHS = (size_t)d.batch * d.n_head * d.seq;
+    const size_t XE = E + 8, XF = F + 8;
+    P->XE = (int)XE;
+    P->XF = (int)XF;
     Carver c{base};
     P->resid_v.assign(3 * L + 1, nullptr);
     for (size_t i = 0; i < 3 * L + 1; ++i) P->resid_v[i] = c.take<float>(T * E);
     P->la.assign(L, LayerActs{});
     for (size_t l = 0; l < L; ++l) {
         LayerActs& a = P->la[l];
-        a.ln1 = c.take<__bf16>(T * E); a.lnx = c.take<__bf16>(T * E); a.ln2 = c.take<__bf16>(T * E);
+        a.ln1 = c.take<__bf16>(T * XE); a.lnx = c.take<__bf16>(T * XE); a.ln2 = c.take<__bf16>(T * XE);
         a.m1 = c.take<float>(T); a.r1 = c.take<float>(T); a.mx = c.take<float>(T);
         a.rx = c.take<float>(T); a.m2 = c.take<float>(T); a.r2 = c.take<float>(T);
-        a.qkv = c.take<__bf16>(T * 3 * E); a.ao = c.take<__bf16>(T * E);
-        a.xq = c.take<__bf16>(T * E); a.xo = c.take<__bf16>(T * E);
-        a.pre = c.take<__bf16>(T * F); a.act = c.take<__bf16>(T * F);
+        a.qkv = c.take<__bf16>(T * 3 * E); a.ao = c.take<__bf16>(T * XE);
+        a.xq = c.take<__bf16>(T * E); a.xo = c.take<__bf16>(T * XE);
+        a.pre = c.take<__bf16>(T * F); a.act = c.take<__bf16>(T * XF);
         a.lse = c.take<float>(BHS); a.xlse = c.take<float>(BHS);
     }
-    P->cap = c.take<__bf16>(T * E);
+    P->cap = c.take<__bf16>(T * XE);
     P->kv_all = c.take<__bf16>(T * 2 * E * L);
     P->lnf = c.take<__bf16>(T * E);
     P->mf = c.take<float>(T); P->rf = c.take<float>(T);
     P->dlogits = c.take<__bf16>(T * d.vocab_pad);
     P->row_loss = c.take<float>(T);
     P->emo_sum = c.take<float>(4);
-    P->emo_tmp = c.take<float>((size_t)d.batch * 7 + 4);
+    P->emo_tmp = c.take<float>((size_t)d.batch * 16 + 8);
     P->n_valid_local = c.take<int>(4);
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
@@ -142,6 +158,18 @@ int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, i
     ERGM_TRY(ws_need(P, ergm_colsum_workspace_size(rows, cols)));
     if (P->dry) return ERGM_OK;
     return ergm_colsum(X, dt, rows, cols, ldx, out, 0, P->scratch, P->scratch_bytes, s);
+}
+
+// Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]).
+// With fused_bias the A operand's column M is all ones and gB == gW + M·N, so one GEMM over M+1
+// rows writes [gW; gB]; otherwise the bias gradient is a separate column sum of dY.
+int dw_gemm(ergm_model_plan* P, hipStream_t s, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
+            float* gW, float* gB) {
+    const int T = P->T;
+    if (P->fused_bias)
+        return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
+    ERGM_TRY(gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE));
+    return colsum(P, s, dY, ERGM_BF16, T, N, ldy, gB);
 }
 
 int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
@@ -191,6 +219,7 @@ extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     P.L2E = 2 * dims->n_embd * dims->n_layer;
     size_t act = carve(&P, nullptr);
     P.dry = true;
+    P.fused_bias = false;  // the colsum fallback needs the larger scratch
     P.need = ergm_embed_bwd_workspace_size(P.T);
     P.need = std::max(P.need, ergm_colsum_workspace_size(P.T, std::max(P.L2E, dims->n_inner)));
     P.labels = P.emo_labels = nullptr;
@@ -228,6 +257,31 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->dry = false;
     P->need = 0;
     P->have_fwd = false;
+    // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py
+    // lays the flat buffers out that way); otherwise fall back to separate column sums.
+    {
+        const int64_t E = d.n_embd, F = d.n_inner;
+        const int64_t* o = P->p.layer_off;
+        auto follows = [&](int w, int b, int64_t K, int64_t N) { return o[b] == o[w] + K * N; };
+        P->fused_bias = follows(ERGM_T_ATTN_W, ERGM_T_ATTN_B, E, 3 * E) && follows(ERGM_T_APROJ_W, ERGM_T_APROJ_B, E, E) &&
+                        follows(ERGM_T_XQ_W, ERGM_T_XQ_B, E, E) && follows(ERGM_T_XPROJ_W, ERGM_T_XPROJ_B, E, E) &&
+                        follows(ERGM_T_FC_W, ERGM_T_FC_B, E, F) && follows(ERGM_T_MPROJ_W, ERGM_T_MPROJ_B, F, E) &&
+                        P->p.g_capkv_b == P->p.g_capkv_w + E * P->L2E;
+        // the ones columns are never overwritten by the producers (they write columns < E / < F)
+        int rc = ERGM_OK;
+        for (int l = 0; l < d.n_layer && rc == ERGM_OK; ++l) {
+            LayerActs& a = P->la[l];
+            const void* cols[5] = {a.ln1, a.lnx, a.ln2, a.ao, a.xo};
+            for (int i = 0; i < 5 && rc == ERGM_OK; ++i) rc = fill_ones_col((void*)cols[i], P->T, P->XE, d.n_embd, nullptr);
+            if (rc == ERGM_OK) rc = fill_ones_col(a.act, P->T, P->XF, d.n_inner, nullptr);
+        }
+        if (rc == ERGM_OK) rc = fill_ones_col(P->cap, P->T, P->XE, d.n_embd, nullptr);
+        if (rc == ERGM_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = fail(ERGM_EHIP, "model_create: sync");
+        if (rc != ERGM_OK) {
+            delete P;
+            return rc;
+        }
+    }
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
     P->n_valid = nullptr;
@@ -274,12 +328,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     const ergm_model_params& p = P->p;
 
     if (!P->dry)
-        ERGM_TRY(ergm_embed_fwd(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap, B,
-                            S, E, d.vocab, s));
+        ERGM_TRY(embed_fwd_ld(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap,
+                              P->XE, B, S, E, d.vocab, s));
     // all L cross-attention K/V projections of the caption embeddings in one GEMM
     {
     Probe pr(P, 4, s);
-    ERGM_TRY(gemm(P, s, T, L2E, E, P->cap, E, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
+    ERGM_TRY(gemm(P, s, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
                   ERGM_EPI_BIAS, p.capkv_b));
     }
     for (int l = 0; l < L; ++l) {
@@ -290,29 +344,33 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         float* x3 = P->resid[3 * l + 3];
         // self-attention sub-block (src/model.py:297-309)
         if (!P->dry)
-            ERGM_TRY(ergm_layernorm_fwd(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, a.m1, a.r1, T, E, d.eps, s));
-        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
+            ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
+                                      d.eps, s));
+        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
                       ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
         if (!P->dry)
-            ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, B, H, S, S, 3 * E, 3 * E, 3 * E, E, 1, s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.ao, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
+            ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
+                                   s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
         // cross-attention over caption embeddings (src/model.py:311-329)
         if (!P->dry)
-            ERGM_TRY(ergm_layernorm_fwd(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, a.mx, a.rx, T, E, d.eps, s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
+            ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
+                                      d.eps, s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
                       ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
         if (!P->dry)
-            ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, E, 0, s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.xo, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
+            ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, P->XE, 0, s));
+        ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
         // MLP (src/model.py:331-334, 262-267)
         if (!P->dry)
-            ERGM_TRY(ergm_layernorm_fwd(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, a.m2, a.r2, T, E, d.eps, s));
-        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, E, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, F, ERGM_BF16,
+            ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
+                                      d.eps, s));
+        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF, ERGM_BF16,
                       ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-        ERGM_TRY(gemm(P, s, T, E, F, a.act, F, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
+        ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
     }
     if (!P->dry)
@@ -324,8 +382,8 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                       ERGM_BF16, ERGM_EPI_NONE));
     }
     if (P->dry) return ERGM_OK;
-    ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, B, S, E, 7,
-                               P->B_global, nullptr, s));
+    ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, P->emo_tmp,
+                               B, S, E, 7, P->B_global, nullptr, s));
     if (P->labels) {
         ERGM_TRY(ergm_xent_fwd_bwd(logits, d.vocab_pad, P->labels, P->n_valid, P->row_loss, train ? P->dlogits : nullptr,
                                    B, S, d.vocab, 1.0f, s));
@@ -371,8 +429,8 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     }
     if (P->dry) return ERGM_OK;
     if (P->emo_labels) {
-        ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w, P->dy, B,
-                                   S, E, 7, P->B_global, gscale, s));
+        ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w,
+                                   P->dy, P->emo_tmp + (size_t)B * 8 + 4, B, S, E, 7, P->B_global, gscale, s));
     } else {
         if (hipMemsetAsync(p.g_emo_w, 0, (size_t)7 * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
     }
@@ -388,48 +446,36 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     const float* x1 = P->dry ? nullptr : P->resid[3 * l + 1];
     const float* x2 = P->dry ? nullptr : P->resid[3 * l + 2];
     // ---- MLP: x3 = x2 + gelu(ln2(x2)·Wfc + bfc)·Wm + bm
-    ERGM_TRY(gemm(P, s, F, E, T, a.act, F, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_MPROJ_W), E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_MPROJ_B)));
+    ERGM_TRY(dw_gemm(P, s, F, E, a.act, P->XF, P->dh_b, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
     ERGM_TRY(gemm(P, s, T, F, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK, P->dpre, F, ERGM_BF16,
                   ERGM_EPI_GELU_BWD, nullptr, a.pre, F));
-    ERGM_TRY(gemm(P, s, E, F, T, a.ln2, E, ERGM_KM, P->dpre, F, ERGM_KN, LG(P, l, ERGM_T_FC_W), F, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dpre, ERGM_BF16, T, F, F, LG(P, l, ERGM_T_FC_B)));
+    ERGM_TRY(dw_gemm(P, s, E, F, a.ln2, P->XE, P->dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
     ERGM_TRY(gemm(P, s, T, E, F, P->dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
     ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
     // ---- cross-attention: x2 = x1 + Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp
-    ERGM_TRY(gemm(P, s, E, E, T, a.xo, E, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_XPROJ_W), E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_XPROJ_B)));
+    ERGM_TRY(dw_gemm(P, s, E, E, a.xo, P->XE, P->dh_b, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
                   ERGM_EPI_NONE));
     if (!P->dry) {
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
         __bf16* dkl = P->dkv_all + (size_t)l * 2 * E;
         ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, P->dxq, dkl, dkl + E, B, H, S, S, E,
-                               L2E, L2E, E, E, E, L2E, L2E, 0, s));
+                               L2E, L2E, P->XE, E, E, L2E, L2E, 0, s));
     }
-    ERGM_TRY(gemm(P, s, E, E, T, a.lnx, E, ERGM_KM, P->dxq, E, ERGM_KN, LG(P, l, ERGM_T_XQ_W), E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dxq, ERGM_BF16, T, E, E, LG(P, l, ERGM_T_XQ_B)));
+    ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, P->dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, P->dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
     ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
     // ---- self-attention: x1 = x0 + Attn(ln_1(x0)·Wqkv + b)·Wap + bap
-    ERGM_TRY(gemm(P, s, E, E, T, a.ao, E, ERGM_KM, P->dh_b, E, ERGM_KN, LG(P, l, ERGM_T_APROJ_W), E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dh, ERGM_F32, T, E, E, LG(P, l, ERGM_T_APROJ_B)));
+    ERGM_TRY(dw_gemm(P, s, E, E, a.ao, P->XE, P->dh_b, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
                   ERGM_EPI_NONE));
     if (!P->dry) {
         ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, P->dqkv, P->dqkv + E,
-                               P->dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, E, E, 3 * E, 3 * E, 3 * E, 1, s));
+                               P->dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, s));
     }
-    ERGM_TRY(gemm(P, s, E, 3 * E, T, a.ln1, E, ERGM_KM, P->dqkv, 3 * E, ERGM_KN, LG(P, l, ERGM_T_ATTN_W), 3 * E,
-                  ERGM_F32, ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dqkv, ERGM_BF16, T, 3 * E, 3 * E, LG(P, l, ERGM_T_ATTN_B)));
+    ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, P->dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
     ERGM_TRY(gemm(P, s, T, E, 3 * E, P->dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
                   ERGM_F32, ERGM_EPI_NONE));
     return ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B));
@@ -440,9 +486,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, L2E = P->L2E;
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all, dcap = dKV_all·Wᵀ
-    ERGM_TRY(gemm(P, s, E, L2E, T, P->cap, E, ERGM_KM, P->dkv_all, L2E, ERGM_KN, p.g_capkv_w, L2E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(colsum(P, s, P->dkv_all, ERGM_BF16, T, L2E, L2E, p.g_capkv_b));
+    ERGM_TRY(dw_gemm(P, s, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));
     if (P->dry) return ERGM_OK;

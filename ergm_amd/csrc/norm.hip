@@ -9,13 +9,13 @@
 
 namespace ergm {
 
-constexpr int LN_ROWS_PER_BLOCK_BWD = 32;
+constexpr int LN_ROWS_PER_BLOCK_BWD = 8;
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, __bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int rows, int E, float eps) {
+                                                     int rows, int E, int ldy, float eps) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
             o[1] = f2bf((v[i].y - mean) * rstd * g.y + b.y);
             o[2] = f2bf((v[i].z - mean) * rstd * g.z + b.z);
             o[3] = f2bf((v[i].w - mean) * rstd * g.w + b.w);
-            *reinterpret_cast<bf16x4*>(y + (size_t)row * E + c) = o;
+            *reinterpret_cast<bf16x4*>(y + (size_t)row * ldy + c) = o;
         }
     }
     if (lane == 0) {
@@ -138,6 +138,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
         part_g[(size_t)blockIdx.x * E + c] = a;
         part_b[(size_t)blockIdx.x * E + c] = b;
     }
+}
+
+// dγ / dβ: sum the per-block partials (fixed order).  grid (cdiv(E,64), 2): 64 columns x 4 row lanes.
+__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ part_g,
+                                                              const float* __restrict__ part_b, int nparts, int E,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ float red[4][64];
+    const float* part = blockIdx.y == 0 ? part_g : part_b;
+    float* out = blockIdx.y == 0 ? dgamma : dbeta;
+    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (c < E) {
+        int r = rl;
+        for (; r + 12 < nparts; r += 16) {
+            s0 += part[(size_t)r * E + c];
+            s1 += part[(size_t)(r + 4) * E + c];
+            s2 += part[(size_t)(r + 8) * E + c];
+            s3 += part[(size_t)(r + 12) * E + c];
+        }
+        for (; r < nparts; r += 4) s0 += part[(size_t)r * E + c];
+    }
+    red[rl][cl] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (rl == 0 && c < E) out[c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 // ---- column sums: out[c] (+)= Σ_r X[r][c] -------------------------------------------------
@@ -226,26 +251,51 @@ size_t colsum_ws(int rows, int cols) {
 
 using namespace ergm;
 
-extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
-                                  float* rstd, int rows, int E, float eps, void* stream) {
+namespace ergm {
+int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
+                     int rows, int E, float eps, hipStream_t s) {
     ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_fwd: unsupported E=%d", E);
+    ERGM_CHECK_ARG(ldy >= E && ldy % 4 == 0, "layernorm_fwd: bad ldy");
     dim3 grid(cdiv(rows, 4));
-    hipStream_t s = as_stream(stream);
     int nv = cdiv(E, 256);
     auto* yb = reinterpret_cast<__bf16*>(y);
     switch (nv) {
-        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
-        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
-        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
-        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, eps); break;
+        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
+        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
+        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
+        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
     }
     return check_launch("layernorm_fwd");
 }
 
+// p[r*ld + col] = 1, p[r*ld + col+1 .. col+7] = 0: the constant "ones" column that turns a weight-
+// gradient GEMM Xᵀ·dY into [dW; db] (row K of the augmented product is Σ_t dY[t]).
+__global__ void ones_col_kernel(__bf16* p, int rows, int ld, int col) {
+    int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f2bf(j == 0 ? 1.f : 0.f);
+    *reinterpret_cast<bf16x8*>(p + (size_t)r * ld + col) = v;
+}
+
+int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s) {
+    ERGM_CHECK_ARG(p && rows > 0 && col % 8 == 0 && ld >= col + 8, "fill_ones_col: bad argument");
+    hipLaunchKernelGGL(ones_col_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, s, reinterpret_cast<__bf16*>(p), rows, ld,
+                       col);
+    return check_launch("fill_ones_col");
+}
+}  // namespace ergm
+
+extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
+                                  float* rstd, int rows, int E, float eps, void* stream) {
+    return layernorm_fwd_ld(x, gamma, beta, y, E, mean, rstd, rows, E, eps, as_stream(stream));
+}
+
 extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {
     int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
-    return 2 * (size_t)nb * E * sizeof(float) + colsum_ws(nb, E);
+    return 2 * (size_t)nb * E * sizeof(float);
 }
 
 extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
@@ -257,8 +307,6 @@ extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* 
     int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
-    float* cws = pb + (size_t)nb * E;
-    size_t cws_bytes = ws_bytes - 2 * (size_t)nb * E * sizeof(float);
     hipStream_t s = as_stream(stream);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     int nv = cdiv(E, 256);
@@ -268,9 +316,8 @@ extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* 
         case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
         default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
     }
-    ERGM_TRY(check_launch("layernorm_bwd"));
-    ERGM_TRY(colsum_impl(pg, false, nb, E, E, dgamma, 0, cws, cws_bytes, s));
-    return colsum_impl(pb, false, nb, E, E, dbeta, 0, cws, cws_bytes, s);
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2), dim3(256), 0, s, pg, pb, nb, E, dgamma, dbeta);
+    return check_launch("layernorm_bwd");
 }
 
 extern "C" size_t ergm_colsum_workspace_size(int rows, int cols) { return colsum_ws(rows, cols); }

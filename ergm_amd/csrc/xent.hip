@@ -112,61 +112,76 @@ __global__ __launch_bounds__(256) void count_valid_kernel(const int64_t* __restr
     if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
 }
 
-// Single workgroup: emotion logits (f32) + CE + gradients.  C ≤ 16, B ≤ 256.
-__global__ __launch_bounds__(256) void emotion_kernel(const __bf16* __restrict__ h, const float* __restrict__ W,
-                                                      const int64_t* __restrict__ labels, float* __restrict__ logits,
-                                                      float* __restrict__ loss_sum, float* __restrict__ dW,
-                                                      float* __restrict__ dh, int B, int S, int E, int C, int B_global,
-                                                      const float* __restrict__ gscale) {
-    extern __shared__ float sm[];
-    float* lg = sm;            // [B][C] logits
-    float* dl = sm + B * C;    // [B][C] dlogits
+// Emotion head, one workgroup per sample b: logits[b][c] = h[b,S-1,:]·W[c,:]; with labels the row
+// loss and dlogits go to `scratch` ([B][C] dlogits then [B] row losses) and, with dh,
+// dh[b,S-1,:] += dlogits[b]·W.
+__global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restrict__ h, const float* __restrict__ W,
+                                                          const int64_t* __restrict__ labels, float* __restrict__ logits,
+                                                          float* __restrict__ scratch, float* __restrict__ dh, int B, int S,
+                                                          int E, int C, int B_global, const float* __restrict__ gscale) {
+    __shared__ float lg[16], dl[16];
+    const int b = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int pc = wave; pc < B * C; pc += 4) {
-        int b = pc / C, c = pc % C;
-        const __bf16* hr = h + ((size_t)b * S + S - 1) * E;
+    const __bf16* hr = h + ((size_t)b * S + S - 1) * E;
+    for (int c = wave; c < C; c += 4) {
         const float* wr = W + (size_t)c * E;
         float acc = 0.f;
         for (int e = lane; e < E; e += 64) acc += bf2f(hr[e]) * wr[e];
         acc = wave_sum(acc);
         if (lane == 0) {
-            lg[pc] = acc;
-            logits[pc] = acc;
+            lg[c] = acc;
+            logits[(size_t)b * C + c] = acc;
         }
     }
     __syncthreads();
     if (!labels) return;
-    const float gs = gscale ? *gscale : 1.f;
-    if (threadIdx.x < B) {
-        int b = threadIdx.x;
+    if (threadIdx.x == 0) {
+        const float gs = gscale ? *gscale : 1.f;
         float mx = -INFINITY;
-        for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[b * C + c]);
+        for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[c]);
         float se = 0.f;
-        for (int c = 0; c < C; ++c) se += expf(lg[b * C + c] - mx);
-        int y = (int)labels[b];
-        for (int c = 0; c < C; ++c)
-            dl[b * C + c] = (expf(lg[b * C + c] - mx) / se - (c == y ? 1.f : 0.f)) * gs / (float)B_global;
-        lg[b * C + 0] = (mx + logf(se)) - lg[b * C + y];  // reuse slot 0 for the row loss
+        for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
+        const int y = (int)labels[b];
+        for (int c = 0; c < C; ++c) {
+            float d = (expf(lg[c] - mx) / se - (c == y ? 1.f : 0.f)) * gs / (float)B_global;
+            dl[c] = d;
+            scratch[(size_t)b * C + c] = d;
+        }
+        scratch[(size_t)B * C + b] = (mx + logf(se)) - lg[y];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (!dh) return;
+    for (int e = threadIdx.x; e < E; e += 256) {
+        float acc = 0.f;
+        for (int c = 0; c < C; ++c) acc += dl[c] * W[(size_t)c * E + e];
+        dh[((size_t)b * S + S - 1) * E + e] += acc;
+    }
+}
+
+// dW[c][e] = Σ_b dlogits[b][c]·h[b,S-1,e] (fixed b order); block 0 also sums the row losses.
+__global__ __launch_bounds__(256) void emotion_dw_kernel(const __bf16* __restrict__ h, const float* __restrict__ scratch,
+                                                         float* __restrict__ loss_sum, float* __restrict__ dW, int B,
+                                                         int S, int E, int C) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         float s = 0.f;
-        for (int b = 0; b < B; ++b) s += lg[b * C];
+        for (int b = 0; b < B; ++b) s += scratch[(size_t)B * C + b];
         *loss_sum = s;
     }
     if (!dW) return;
-    for (int i = threadIdx.x; i < C * E; i += 256) {
-        int c = i / E, e = i % E;
-        float acc = 0.f;
-        for (int b = 0; b < B; ++b) acc += dl[b * C + c] * bf2f(h[((size_t)b * S + S - 1) * E + e]);
-        dW[i] = acc;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    float acc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    for (int b = 0; b < B; ++b) {
+        float hv = bf2f(h[((size_t)b * S + S - 1) * E + e]);
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            if (c < C) acc[c] += scratch[(size_t)b * C + c] * hv;
     }
-    for (int i = threadIdx.x; i < B * E; i += 256) {
-        int b = i / E, e = i % E;
-        float acc = 0.f;
-        for (int c = 0; c < C; ++c) acc += dl[b * C + c] * W[(size_t)c * E + e];
-        dh[((size_t)b * S + S - 1) * E + e] += acc;
-    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+        if (c < C) dW[(size_t)c * E + e] = acc[c];
 }
 
 __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restrict__ row_loss, int T,
@@ -213,16 +228,21 @@ extern "C" int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* lab
 }
 
 extern "C" int ergm_emotion_head(const void* h, const float* W, const int64_t* labels, float* logits, float* loss_sum,
-                                 float* dW, float* dh, int B, int S, int E, int C, int B_global,
+                                 float* dW, float* dh, float* scratch, int B, int S, int E, int C, int B_global,
                                  const float* grad_scale_dev, void* stream) {
     ERGM_CHECK_ARG(h && W && logits, "emotion_head: null argument");
-    ERGM_CHECK_ARG(B > 0 && B <= 256 && C > 0 && C <= 16 && E > 0 && S > 0, "emotion_head: bad shape");
-    ERGM_CHECK_ARG(!labels || loss_sum, "emotion_head: labels need loss_sum");
+    ERGM_CHECK_ARG(B > 0 && C > 0 && C <= 16 && E > 0 && S > 0, "emotion_head: bad shape");
+    ERGM_CHECK_ARG(!labels || (loss_sum && scratch), "emotion_head: labels need loss_sum and scratch");
     ERGM_CHECK_ARG((dW == nullptr) == (dh == nullptr), "emotion_head: dW and dh go together");
     ERGM_CHECK_ARG(!dW || labels, "emotion_head: gradients need labels");
-    size_t lds = 2 * (size_t)B * C * sizeof(float);
-    hipLaunchKernelGGL(emotion_kernel, dim3(1), dim3(256), lds, as_stream(stream), reinterpret_cast<const __bf16*>(h),
-                       W, labels, logits, loss_sum, dW, dh, B, S, E, C, B_global > 0 ? B_global : B, grad_scale_dev);
+    hipStream_t s = as_stream(stream);
+    const __bf16* hb = reinterpret_cast<const __bf16*>(h);
+    const int bg = B_global > 0 ? B_global : B;
+    hipLaunchKernelGGL(emotion_row_kernel, dim3(B), dim3(256), 0, s, hb, W, labels, logits, scratch, dh, B, S, E, C, bg,
+                       grad_scale_dev);
+    if (labels)
+        hipLaunchKernelGGL(emotion_dw_kernel, dim3(dW ? cdiv(E, 256) : 1), dim3(256), 0, s, hb, scratch, loss_sum, dW,
+                           B, S, E, C);
     return check_launch("emotion_head");
 }
 

@@ -164,8 +164,9 @@ def emotion_head(h, W, labels, B, S, B_global=None, dh=None, grad_scale=None):
     logits = torch.empty(B, Cn, dtype=torch.float32, device=h.device)
     loss_sum = torch.empty(1, dtype=torch.float32, device=h.device)
     dW = torch.empty_like(W) if dh is not None else None
-    L.call("ergm_emotion_head", _ptr(h), _ptr(W), _ptr(labels), _ptr(logits), _ptr(loss_sum), _ptr(dW), _ptr(dh), B, S,
-           E, Cn, B_global or B, _ptr(grad_scale), _stream(h.device))
+    scratch = torch.empty(B * (Cn + 1), dtype=torch.float32, device=h.device)
+    L.call("ergm_emotion_head", _ptr(h), _ptr(W), _ptr(labels), _ptr(logits), _ptr(loss_sum), _ptr(dW), _ptr(dh),
+           _ptr(scratch), B, S, E, Cn, B_global or B, _ptr(grad_scale), _stream(h.device))
     return logits, loss_sum, dW
 
 

@@ -147,10 +147,11 @@ int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* labels, const 
                       float* row_loss, void* dlogits, int B, int S, int V, float grad_scale,
                       void* stream);
 /* Emotion head on the last token: logits[b][c] = Σ_e h[b,S-1,e]·W[c][e] (h bf16, W f32 [C][E]);
- * if labels: loss_out = mean CE over B_global (loss_sum written), dW[C][E] written,
- * dh[b,S-1,:] += dlogits·W (f32 dh [B*S][E]).                                                   */
+ * with labels: loss_sum = Σ_b CE_b (the caller divides by B_global), scratch = B*(C+1) floats; with
+ * dW/dh: dW[C][E] written and dh[b,S-1,:] += dlogits·W (f32 dh [B*S][E]), dlogits =
+ * (softmax - onehot)·grad_scale/B_global.                                                       */
 int ergm_emotion_head(const void* h, const float* W, const int64_t* labels, float* logits,
-                      float* loss_sum, float* dW, float* dh, int B, int S, int E, int C,
+                      float* loss_sum, float* dW, float* dh, float* scratch, int B, int S, int E, int C,
                       int B_global, const float* grad_scale_dev, void* stream);
 /* out[0] = Σ row_loss / n_valid_global (0 if n_valid_global is NULL), out[1] = emo_loss_sum / B_global, out[2] = out[0]+out[1]. */
 int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
