@@ -242,6 +242,159 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
             }
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined variant: NS-stage LDS ring filled by global_load_lds_dwordx4 (LDS-DMA, no VGPR staging).
+// The DMA writes each wave-instruction's 64 x 16 B lane-linearly, so the XOR swizzles above are applied
+// to the per-lane SOURCE address (same involution on the read).  Stage kt is consumed after a counted
+// s_waitcnt vmcnt (the younger stages stay in flight) and a raw s_barrier; the freed slot is refilled
+// right after that barrier.  Out-of-range rows/columns are CLAMPED to valid memory (never masked), so
+// every wave issues the same number of DMA instructions per stage and the counts stay exact; clamped
+// data only reaches output rows/columns that are not stored.  Requires K % 64 == 0.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One 16-B-per-lane LDS-DMA: LDS[lds_addr + 16*lane] = *gsrc.  Issued from inline asm so hipcc does
+// not track it (it would otherwise drain vmcnt before every later ds_read); completion is covered by
+// the explicit counted waits.  M0 is saved/set/restored inside the one statement (guide §5.7).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int ROWS, bool TRANS>
+struct GldsTile {
+    static constexpr int BYTES = ROWS * GEMM_BK * 2;
+    static constexpr int PER_WAVE = BYTES / 1024 / 4;   // wave-instructions per wave per stage
+    static constexpr int CPR = TRANS ? ROWS / 8 : 8;
+    static constexpr int ROW_BYTES = CPR * 16;
+    static_assert(PER_WAVE >= 1, "tile too small for 4-wave LDS-DMA staging");
+
+    // r0: tile origin along M|N; Rlim: M|N (valid extent); k0: K origin of the stage.
+    __device__ __forceinline__ static void issue(char* lds, const __bf16* base, int ld, int r0, int Rlim, int k0,
+                                                 int wave) {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int i = 0; i < PER_WAVE; ++i) {
+            const int ib = (i * 4 + wave) * 1024;
+            const int o = ib + lane * 16;
+            const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
+            const __bf16* src;
+            if (!TRANS) {
+                const int c = pc ^ swz_row(row);
+                const int r = min(r0 + row, Rlim - 1);
+                src = base + (size_t)r * ld + k0 + c * 8;
+            } else {
+                const int c = pc ^ (CPR == 16 ? swz_tr16(row) : swz_tr8(row));
+                const int col = min(r0 + c * 8, ((Rlim + 7) & ~7) - 8);
+                src = base + (size_t)(k0 + row) * ld + col;
+            }
+            glds16(src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + ib)));
+        }
+    }
+};
+
+template <int BM, int BN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
+    constexpr int STAGE = A_BYTES + B_BYTES;
+    constexpr int LPS = GldsTile<BM, A_KM>::PER_WAVE + GldsTile<BN, B_KN>::PER_WAVE;  // vmcnt per stage
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int id = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = blockIdx.z * a.k_per_split;
+    const int kend = min(a.K, kbeg + a.k_per_split);
+    const int nk = (kend - kbeg) / GEMM_BK;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_stage = [&](int kt) {
+        char* st = smem + (kt % NS) * STAGE;
+        const int k0 = kbeg + kt * GEMM_BK;
+        GldsTile<BM, A_KM>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
+        GldsTile<BN, B_KN>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
+    };
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue_stage(s);
+
+    TileLoader<BM, A_KM> la;  // fragment readers (same LDS image / swizzle as the register path)
+    TileLoader<BN, B_KN> lb;
+    for (int kt = 0; kt < nk; ++kt) {
+        // stages issued after kt by this wave: min(NS-2, nk-1-kt)
+        const int after = min(NS - 2, nk - 1 - kt);
+        if (after >= 2) wait_vm<2 * LPS>();
+        else if (after == 1) wait_vm<LPS>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+        const char* st = smem + (kt % NS) * STAGE;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fa[FM], fb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    const int lane = threadIdx.x & 63;
+    const int rbase = m0 + wm * WM + (lane >> 4) * 4;
+    const int cbase = n0 + wn * WN + (lane & 15);
+    if (a.slab) {
+        float* slab = a.slab + (size_t)blockIdx.z * a.M * a.N;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int m = rbase + i * 16 + r, n = cbase + j * 16;
+                    if (m < a.M && n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][r];
+                }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = rbase + i * 16 + r, n = cbase + j * 16;
+                if (m < a.M && n < a.N) epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
+            }
+}
+
 // split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
 template <int EPI, bool OUT_BF16>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int splits) {
@@ -294,8 +447,25 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
 
 template <int BM, int BN, bool AKM, bool BKN, int EPI, bool OB>
 static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
-    constexpr size_t lds = 2 * (BM + BN) * GEMM_BK * 2;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
+    const bool pipe = a.K % GEMM_BK == 0 && a.k_per_split % GEMM_BK == 0;
+    if (pipe) {
+        constexpr int NS = (BM + BN) >= 256 ? 3 : 4;
+        constexpr size_t lds = (size_t)NS * (BM + BN) * GEMM_BK * 2;
+        if (split > 1) {
+            auto k = gemm_pipe_kernel<BM, BN, NS, AKM, BKN, ERGM_EPI_NONE, false>;
+            static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
+            (void)attr;
+            hipLaunchKernelGGL(k, grid, dim3(GEMM_THREADS), lds, s, a);
+        } else {
+            auto k = gemm_pipe_kernel<BM, BN, NS, AKM, BKN, EPI, OB>;
+            static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
+            (void)attr;
+            hipLaunchKernelGGL(k, grid, dim3(GEMM_THREADS), lds, s, a);
+        }
+        return;
+    }
+    constexpr size_t lds = 2 * (BM + BN) * GEMM_BK * 2;
     if (split > 1) {
         // raw partials: epilogue handled by splitk_reduce_kernel
         hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
