@@ -141,6 +141,95 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
     }
 }
 
+// Vectorized epilogue for 8 consecutive columns n..n+7 of row m (N % 8 == 0, n % 8 == 0).
+template <int EPI, bool OUT_BF16>
+__device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n, float* v) {
+    if (EPI == ERGM_EPI_BIAS || EPI == ERGM_EPI_BIAS_GELU || EPI == ERGM_EPI_BIAS_RESID) {
+        if (a.bias) {
+            float4 b0 = *reinterpret_cast<const float4*>(a.bias + n);
+            float4 b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+    }
+    if (EPI == ERGM_EPI_BIAS_GELU) {
+        bf16x8 pre;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            pre[j] = f2bf(v[j]);
+            v[j] = gelu_new(v[j]);
+        }
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.aux_out) + (size_t)m * a.ld_aux_out + n) = pre;
+    } else if (EPI == ERGM_EPI_BIAS_RESID) {
+        const float* r = reinterpret_cast<const float*>(a.aux) + (size_t)m * a.ld_aux + n;
+        float4 r0 = *reinterpret_cast<const float4*>(r), r1 = *reinterpret_cast<const float4*>(r + 4);
+        v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+        v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    } else if (EPI == ERGM_EPI_GELU_BWD) {
+        bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.aux) + (size_t)m * a.ld_aux + n);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_new_grad(bf2f(x[j]));
+    }
+    const size_t idx = (size_t)m * a.ldc + n;
+    if (OUT_BF16) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.C) + idx) = o;
+    } else {
+        float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + idx);
+        float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+        if (EPI == ERGM_EPI_ACCUM) {
+            float4 p0 = c[0], p1 = c[1];
+            o0.x += p0.x; o0.y += p0.y; o0.z += p0.z; o0.w += p0.w;
+            o1.x += p1.x; o1.y += p1.y; o1.z += p1.z; o1.w += p1.w;
+        }
+        c[0] = o0;
+        c[1] = o1;
+    }
+}
+
+// Write a BM x BN accumulator tile (4 waves as 2x2, 16x16 MFMA fragments) through LDS so that every
+// global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
+// (the per-lane form made the large GEMMs store-issue bound).  `lds` must hold BM*(BN+4) floats and
+// be free (call after the main loop's last barrier).  slab != nullptr: raw f32 split-K partials.
+template <int BM, int BN, int EPI, bool OUT_BF16, int FM, int FN>
+__device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
+                                           float alpha, float* slab) {
+    constexpr int LD = BN + 4;  // rows 16 B apart mod 32 banks: lanes l and l+16 hit disjoint banks
+    constexpr int WM = BM / 2, WN = BN / 2;
+    float* t = reinterpret_cast<float*>(lds);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                t[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 8-column chunks per row
+    for (int c = threadIdx.x; c < BM * CPR; c += GEMM_THREADS) {
+        const int row = c / CPR, col = (c % CPR) * 8;
+        const int m = m0 + row, n = n0 + col;
+        if (m >= a.M || n >= a.N) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
+        const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        if (slab) {
+            float4* d = reinterpret_cast<float4*>(slab + (size_t)m * a.N + n);
+            d[0] = x0;
+            d[1] = x1;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] *= alpha;
+            epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
+        }
+    }
+}
+
 // bijective XCD-grouping remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous range.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int NX = 8;
@@ -216,21 +305,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
-    const int rbase = m0 + wm * WM + (lane >> 4) * 4;
-    const int cbase = n0 + wn * WN + (lane & 15);
-    if (a.slab) {
-        float* slab = a.slab + (size_t)blockIdx.z * a.M * a.N;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int m = rbase + i * 16 + r, n = cbase + j * 16;
-                    if (m < a.M && n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][r];
-                }
+    float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
+    if (a.N % 8 == 0 && (a.slab || a.ldc % 8 == 0)) {
+        store_tile<BM, BN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
         return;
     }
+    const int lane_ = threadIdx.x & 63, wave_ = threadIdx.x >> 6;
+    const int rbase = m0 + (wave_ >> 1) * WM + (lane_ >> 4) * 4;
+    const int cbase = n0 + (wave_ & 1) * WN + (lane_ & 15);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -238,7 +320,9 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 int m = rbase + i * 16 + r, n = cbase + j * 16;
-                if (m < a.M && n < a.N) epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
+                if (m >= a.M || n >= a.N) continue;
+                if (slab) slab[(size_t)m * a.N + n] = acc[i][j][r];
+                else epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
             }
 }
 
@@ -368,22 +452,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
 
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
-    const int lane = threadIdx.x & 63;
-    const int rbase = m0 + wm * WM + (lane >> 4) * 4;
-    const int cbase = n0 + wn * WN + (lane & 15);
-    if (a.slab) {
-        float* slab = a.slab + (size_t)blockIdx.z * a.M * a.N;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int m = rbase + i * 16 + r, n = cbase + j * 16;
-                    if (m < a.M && n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][r];
-                }
+    float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
+    if (a.N % 8 == 0 && (a.slab || a.ldc % 8 == 0)) {
+        store_tile<BM, BN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
         return;
     }
+    const int lane_ = threadIdx.x & 63, wave_ = threadIdx.x >> 6;
+    const int rbase = m0 + (wave_ >> 1) * WM + (lane_ >> 4) * 4;
+    const int cbase = n0 + (wave_ & 1) * WN + (lane_ & 15);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -391,7 +467,9 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 int m = rbase + i * 16 + r, n = cbase + j * 16;
-                if (m < a.M && n < a.N) epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
+                if (m >= a.M || n >= a.N) continue;
+                if (slab) slab[(size_t)m * a.N + n] = acc[i][j][r];
+                else epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
             }
 }
 
@@ -451,7 +529,7 @@ static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
     const bool pipe = a.K % GEMM_BK == 0 && a.k_per_split % GEMM_BK == 0;
     if (pipe) {
         constexpr int NS = (BM + BN) >= 256 ? 3 : 4;
-        constexpr size_t lds = (size_t)NS * (BM + BN) * GEMM_BK * 2;
+        constexpr size_t lds = std::max((size_t)NS * (BM + BN) * GEMM_BK * 2, (size_t)BM * (BN + 4) * 4);
         if (split > 1) {
             auto k = gemm_pipe_kernel<BM, BN, NS, AKM, BKN, ERGM_EPI_NONE, false>;
             static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
@@ -465,7 +543,13 @@ static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
         }
         return;
     }
-    constexpr size_t lds = 2 * (BM + BN) * GEMM_BK * 2;
+    constexpr size_t lds = std::max((size_t)2 * (BM + BN) * GEMM_BK * 2, (size_t)BM * (BN + 4) * 4);
+    static bool attr = (hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AKM, BKN, EPI, OB>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        true);
+    (void)attr;
     if (split > 1) {
         // raw partials: epilogue handled by splitk_reduce_kernel
         hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
