@@ -53,6 +53,7 @@ vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 _SIGS = {
     "ergm_version": (i32, []),
     "ergm_last_error": (i32, [C.c_char_p, sz]),
+    "ergm_gemm_tune": (i32, [i32, i32]),
     "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
     "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),

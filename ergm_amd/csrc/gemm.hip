@@ -189,43 +189,48 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
     }
 }
 
-// Write a BM x BN accumulator tile (4 waves as 2x2, 16x16 MFMA fragments) through LDS so that every
+// Write a BM x BN accumulator tile (WGM x WGN waves, 16x16 MFMA fragments) through LDS so that every
 // global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
-// (the per-lane form made the large GEMMs store-issue bound).  `lds` must hold BM*(BN+4) floats and
-// be free (call after the main loop's last barrier).  slab != nullptr: raw f32 split-K partials.
-template <int BM, int BN, int EPI, bool OUT_BF16, int FM, int FN>
+// (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
+// the staging buffer is (BM/WGM)*(BN+4) floats.  slab != nullptr: raw f32 split-K partials.
+template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
                                            float alpha, float* slab) {
-    constexpr int LD = BN + 4;  // rows 16 B apart mod 32 banks: lanes l and l+16 hit disjoint banks
-    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int LD = BN + 4;  // lanes l and l+16 (rows 4 apart) land 16 banks apart
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int NT = 64 * WGM * WGN;
     float* t = reinterpret_cast<float*>(lds);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wm = wave >> 1, wn = wave & 1;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                t[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
+    const int wm = wave / WGN, wn = wave % WGN;
     constexpr int CPR = BN / 8;  // 8-column chunks per row
-    for (int c = threadIdx.x; c < BM * CPR; c += GEMM_THREADS) {
-        const int row = c / CPR, col = (c % CPR) * 8;
-        const int m = m0 + row, n = n0 + col;
-        if (m >= a.M || n >= a.N) continue;
-        const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
-        const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
-        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        if (slab) {
-            float4* d = reinterpret_cast<float4*>(slab + (size_t)m * a.N + n);
-            d[0] = x0;
-            d[1] = x1;
-        } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] *= alpha;
-            epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
+    for (int pass = 0; pass < WGM; ++pass) {
+        __syncthreads();
+        if (wm == pass) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        t[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < WM * CPR; c += NT) {
+            const int row = c / CPR, col = (c % CPR) * 8;
+            const int m = m0 + pass * WM + row, n = n0 + col;
+            if (m >= a.M || n >= a.N) continue;
+            const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
+            const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
+            if (slab) {
+                float4* d = reinterpret_cast<float4*>(slab + (size_t)m * a.N + n);
+                d[0] = x0;
+                d[1] = x1;
+            } else {
+                float v[8] = {x0.x * alpha, x0.y * alpha, x0.z * alpha, x0.w * alpha,
+                              x1.x * alpha, x1.y * alpha, x1.z * alpha, x1.w * alpha};
+                epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
+            }
         }
     }
 }
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
     if (a.alpha_dev) alpha *= *a.alpha_dev;
     float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
     if (a.N % 8 == 0 && (a.slab || a.ldc % 8 == 0)) {
-        store_tile<BM, BN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
+        store_tile<BM, BN, 2, 2, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
         return;
     }
     const int lane_ = threadIdx.x & 63, wave_ = threadIdx.x >> 6;
@@ -354,13 +359,13 @@ __device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int ROWS, bool TRANS>
+template <int ROWS, bool TRANS, int NWAVES>
 struct GldsTile {
     static constexpr int BYTES = ROWS * GEMM_BK * 2;
-    static constexpr int PER_WAVE = BYTES / 1024 / 4;   // wave-instructions per wave per stage
+    static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;   // wave-instructions per wave per stage
     static constexpr int CPR = TRANS ? ROWS / 8 : 8;
     static constexpr int ROW_BYTES = CPR * 16;
-    static_assert(PER_WAVE >= 1, "tile too small for 4-wave LDS-DMA staging");
+    static_assert(PER_WAVE >= 1 && PER_WAVE * 1024 * NWAVES == BYTES, "tile / wave count mismatch");
 
     // r0: tile origin along M|N; Rlim: M|N (valid extent); k0: K origin of the stage.
     __device__ __forceinline__ static void issue(char* lds, const __bf16* base, int ld, int r0, int Rlim, int k0,
@@ -368,7 +373,7 @@ struct GldsTile {
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int i = 0; i < PER_WAVE; ++i) {
-            const int ib = (i * 4 + wave) * 1024;
+            const int ib = (i * NWAVES + wave) * 1024;
             const int o = ib + lane * 16;
             const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
             const __bf16* src;
@@ -386,13 +391,19 @@ struct GldsTile {
     }
 };
 
-template <int BM, int BN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
-    constexpr int WM = BM / 2, WN = BN / 2;
+// Fragment reader for a staged tile (any wave count): same LDS image and swizzles as TileLoader.
+template <int ROWS, bool TRANS>
+using FragReader = TileLoader<ROWS, TRANS>;
+
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
+    constexpr int NW = WGM * WGN;
+    constexpr int WM = BM / WGM, WN = BN / WGN;
     constexpr int FM = WM / 16, FN = WN / 16;
     constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
     constexpr int STAGE = A_BYTES + B_BYTES;
-    constexpr int LPS = GldsTile<BM, A_KM>::PER_WAVE + GldsTile<BN, B_KN>::PER_WAVE;  // vmcnt per stage
+    constexpr int LPS = GldsTile<BM, A_KM, NW>::PER_WAVE + GldsTile<BN, B_KN, NW>::PER_WAVE;  // vmcnt per stage
+    static_assert(NS >= 2 && NS <= 4, "2..4 stages");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int nwg = a.tiles_m * a.tiles_n;
@@ -405,7 +416,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
     const int kend = min(a.K, kbeg + a.k_per_split);
     const int nk = (kend - kbeg) / GEMM_BK;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WGN, wn = wave % WGN;
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -416,22 +427,22 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
     auto issue_stage = [&](int kt) {
         char* st = smem + (kt % NS) * STAGE;
         const int k0 = kbeg + kt * GEMM_BK;
-        GldsTile<BM, A_KM>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
-        GldsTile<BN, B_KN>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
+        GldsTile<BM, A_KM, NW>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
+        GldsTile<BN, B_KN, NW>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue_stage(s);
 
-    TileLoader<BM, A_KM> la;  // fragment readers (same LDS image / swizzle as the register path)
-    TileLoader<BN, B_KN> lb;
+    FragReader<BM, A_KM> la;
+    FragReader<BN, B_KN> lb;
     for (int kt = 0; kt < nk; ++kt) {
-        // stages issued after kt by this wave: min(NS-2, nk-1-kt)
+        // stages this wave issued after kt: min(NS-2, nk-1-kt); wait until stage kt has landed
         const int after = min(NS - 2, nk - 1 - kt);
         if (after >= 2) wait_vm<2 * LPS>();
         else if (after == 1) wait_vm<LPS>();
         else wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot to refill are done
         __builtin_amdgcn_s_barrier();
         if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
         const char* st = smem + (kt % NS) * STAGE;
@@ -449,28 +460,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_pipe_kernel(GemmArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
     }
-
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
     float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
-    if (a.N % 8 == 0 && (a.slab || a.ldc % 8 == 0)) {
-        store_tile<BM, BN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
-        return;
-    }
-    const int lane_ = threadIdx.x & 63, wave_ = threadIdx.x >> 6;
-    const int rbase = m0 + (wave_ >> 1) * WM + (lane_ >> 4) * 4;
-    const int cbase = n0 + (wave_ & 1) * WN + (lane_ & 15);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int m = rbase + i * 16 + r, n = cbase + j * 16;
-                if (m >= a.M || n >= a.N) continue;
-                if (slab) slab[(size_t)m * a.N + n] = acc[i][j][r];
-                else epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * acc[i][j][r]);
-            }
+    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
 }
 
 // split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
@@ -490,30 +483,73 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int spli
 // ------------------------------------------------------------------------------------------
 // host dispatch
 // ------------------------------------------------------------------------------------------
+// Pipelined-kernel configurations (tile BM x BN, wave grid WGM x WGN, LDS stages NS).
+struct PipeCfg {
+    int bm, bn, wgm, wgn, ns;
+};
+static constexpr PipeCfg kCfgs[] = {
+    {64, 64, 2, 2, 4},     // 0
+    {128, 128, 2, 2, 3},   // 1
+    {128, 128, 2, 2, 2},   // 2
+    {128, 128, 2, 4, 3},   // 3  8 waves (64x32 each)
+    {256, 128, 4, 2, 3},   // 4  8 waves (64x64 each)
+    {128, 256, 2, 4, 3},   // 5  8 waves (64x64 each)
+    {256, 256, 4, 2, 2},   // 6  8 waves (64x128 each)
+    {128, 64, 2, 2, 4},    // 7
+    {64, 128, 2, 2, 4},    // 8
+    {256, 128, 4, 2, 2},   // 9
+    {128, 128, 4, 2, 2},   // 10 8 waves (32x64 each)
+};
+static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+static thread_local int g_force_cfg = -1;    // ergm_gemm_tune: -1 = automatic
+static thread_local int g_force_split = 0;
+
 struct GemmPlan {
-    int bm, bn, split, kps;
+    int cfg;    // index into kCfgs, or -1: register-staged fallback kernel
+    int bm, bn;
+    int split, kps;
 };
 
+static long tiles_of(int M, int N, int bm, int bn) { return (long)cdiv(M, bm) * cdiv(N, bn); }
+
+static bool pipe_ok(const ergm_gemm_desc* d) {
+    // the pipelined path needs K % 64 == 0 and 16-B vector epilogue access (N, ldc, aux lds % 8)
+    return d->K % GEMM_BK == 0 && d->N % 8 == 0 && d->ldc % 8 == 0 && (!d->aux || d->ld_aux % 8 == 0) &&
+           (!d->aux_out || d->ld_aux_out % 8 == 0);
+}
+
 static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
-    // Tile / split-K choice: fill the 256 CUs with >= ~200 workgroups; very deep K (LM-head dX over
-    // the vocabulary, the stacked caption K/V dX) goes to 128x128 tiles split along K.
     GemmPlan p;
     const int M = d->M, N = d->N, K = d->K;
-    const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
-    const long t64 = (long)cdiv(M, 64) * cdiv(N, 64);
     int split = 1;
-    if (t128 >= 240) {
-        p.bm = p.bn = 128;
-    } else if (K >= 4096 && d->split_k != 1) {
-        p.bm = p.bn = 128;
-        split = (int)((512 + t128 - 1) / t128);
-        split = std::max(1, std::min(split, K / 1024));
+    if (!pipe_ok(d)) {
+        p.cfg = -1;
+        const long t128 = tiles_of(M, N, 128, 128), t64 = tiles_of(M, N, 64, 64);
+        p.bm = p.bn = t128 >= 240 ? 128 : 64;
+        if (p.bm == 64 && t64 < 200 && K >= 1024 && d->split_k != 1)
+            split = std::max(1, std::min((int)((400 + t64 - 1) / t64), K / 512));
+    } else if (g_force_cfg >= 0 && g_force_cfg < kNumCfgs) {
+        p.cfg = g_force_cfg;
+        split = std::max(1, g_force_split);
     } else {
-        p.bm = p.bn = 64;
-        if (t64 < 200 && K >= 1024 && d->split_k != 1) {
-            split = (int)((400 + t64 - 1) / t64);
-            split = std::max(1, std::min(split, K / 512));
+        // Tile choice per shape class (measured on MI355X, tools/gemm_tune.py): large outputs take
+        // big 8-wave tiles; the T x E projections take 64x64 / 128x64 tiles; deep K splits.
+        const long t128 = tiles_of(M, N, 128, 128), t64 = tiles_of(M, N, 64, 64);
+        if (t128 >= 240) {
+            p.cfg = 1;
+        } else if (K >= 4096 && d->split_k != 1) {
+            p.cfg = 1;
+            split = std::max(1, std::min((int)((512 + t128 - 1) / t128), K / 1024));
+        } else {
+            p.cfg = 0;
+            if (t64 < 200 && K >= 1024 && d->split_k != 1)
+                split = std::max(1, std::min((int)((400 + t64 - 1) / t64), K / 512));
         }
+    }
+    if (p.cfg >= 0) {
+        p.bm = kCfgs[p.cfg].bm;
+        p.bn = kCfgs[p.cfg].bn;
     }
     if (d->split_k > 1) split = d->split_k;
     int kps = cdiv(cdiv(K, split), GEMM_BK) * GEMM_BK;
@@ -523,26 +559,44 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
     return p;
 }
 
-template <int BM, int BN, bool AKM, bool BKN, int EPI, bool OB>
-static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
+template <int C, bool AKM, bool BKN, int EPI, bool OB>
+static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
+    constexpr PipeCfg c = kCfgs[C];
+    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2,
+                                    (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
+    auto k = split > 1 ? gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>
+                       : gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>;
+    static bool attr = (hipFuncSetAttribute((const void*)gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN,
+                                                                          ERGM_EPI_NONE, false>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        hipFuncSetAttribute((const void*)gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        true);
+    (void)attr;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
-    const bool pipe = a.K % GEMM_BK == 0 && a.k_per_split % GEMM_BK == 0;
-    if (pipe) {
-        constexpr int NS = (BM + BN) >= 256 ? 3 : 4;
-        constexpr size_t lds = std::max((size_t)NS * (BM + BN) * GEMM_BK * 2, (size_t)BM * (BN + 4) * 4);
-        if (split > 1) {
-            auto k = gemm_pipe_kernel<BM, BN, NS, AKM, BKN, ERGM_EPI_NONE, false>;
-            static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
-            (void)attr;
-            hipLaunchKernelGGL(k, grid, dim3(GEMM_THREADS), lds, s, a);
-        } else {
-            auto k = gemm_pipe_kernel<BM, BN, NS, AKM, BKN, EPI, OB>;
-            static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
-            (void)attr;
-            hipLaunchKernelGGL(k, grid, dim3(GEMM_THREADS), lds, s, a);
-        }
-        return;
+    hipLaunchKernelGGL(k, grid, dim3(64 * c.wgm * c.wgn), lds, s, a);
+}
+
+template <bool AKM, bool BKN, int EPI, bool OB>
+static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
+    switch (cfg) {
+        case 0: launch_pipe_cfg<0, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 1: launch_pipe_cfg<1, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 2: launch_pipe_cfg<2, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 3: launch_pipe_cfg<3, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 4: launch_pipe_cfg<4, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 5: launch_pipe_cfg<5, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 6: launch_pipe_cfg<6, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 7: launch_pipe_cfg<7, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 8: launch_pipe_cfg<8, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 9: launch_pipe_cfg<9, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<10, AKM, BKN, EPI, OB>(a, split, s); break;
     }
+}
+
+// register-staged fallback (K % 64 != 0, odd N / leading dims, rarely used layout/epilogue pairs)
+template <int BM, int BN, bool AKM, bool BKN, int EPI, bool OB>
+static void launch_reg(const GemmArgs& a, int split, hipStream_t s) {
     constexpr size_t lds = std::max((size_t)2 * (BM + BN) * GEMM_BK * 2, (size_t)BM * (BN + 4) * 4);
     static bool attr = (hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AKM, BKN, EPI, OB>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -550,24 +604,45 @@ static void launch_t(const GemmArgs& a, int split, hipStream_t s) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         true);
     (void)attr;
-    if (split > 1) {
-        // raw partials: epilogue handled by splitk_reduce_kernel
+    dim3 grid(a.tiles_m * a.tiles_n, 1, split);
+    if (split > 1)
         hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
-    } else {
+    else
         hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, EPI, OB>), grid, dim3(GEMM_THREADS), lds, s, a);
+}
+
+template <bool AKM, bool BKN, int EPI, bool OB>
+static void launch_reg_any(const GemmArgs& a, const GemmPlan& p, hipStream_t s) {
+    if (p.bm == 128) launch_reg<128, 128, AKM, BKN, EPI, OB>(a, p.split, s);
+    else launch_reg<64, 64, AKM, BKN, EPI, OB>(a, p.split, s);
+}
+
+// Layout/epilogue pairs the training step issues get the pipelined kernel family.
+template <bool AKM, bool BKN, int EPI, bool OB>
+static constexpr bool pipe_combo() {
+    return (!AKM && BKN && (EPI == ERGM_EPI_BIAS || EPI == ERGM_EPI_BIAS_GELU) && OB) ||
+           (!AKM && BKN && EPI == ERGM_EPI_BIAS_RESID && !OB) || (!AKM && BKN && EPI == ERGM_EPI_NONE && !OB) ||
+           (!AKM && !BKN && EPI == ERGM_EPI_NONE) || (!AKM && !BKN && EPI == ERGM_EPI_GELU_BWD && OB) ||
+           (AKM && BKN && EPI == ERGM_EPI_NONE && !OB);
+}
+
+template <bool AKM, bool BKN, int EPI, bool OB>
+static void launch_any(const GemmArgs& a, const GemmPlan& p, hipStream_t s) {
+    if constexpr (pipe_combo<AKM, BKN, EPI, OB>()) {
+        if (p.cfg >= 0) {
+            launch_pipe<AKM, BKN, EPI, OB>(a, p.cfg, p.split, s);
+            return;
+        }
     }
+    launch_reg_any<AKM, BKN, EPI, OB>(a, p, s);
 }
 
 template <int EPI, bool OB>
 static void launch_layout(const GemmArgs& a, const GemmPlan& p, int al, int bl, hipStream_t s) {
-#define ERGM_GEMM_LAYOUTS(BM, BN)                                                      \
-    if (al == ERGM_MK && bl == ERGM_NK) launch_t<BM, BN, false, false, EPI, OB>(a, p.split, s); \
-    else if (al == ERGM_MK && bl == ERGM_KN) launch_t<BM, BN, false, true, EPI, OB>(a, p.split, s); \
-    else if (al == ERGM_KM && bl == ERGM_NK) launch_t<BM, BN, true, false, EPI, OB>(a, p.split, s); \
-    else launch_t<BM, BN, true, true, EPI, OB>(a, p.split, s);
-    if (p.bm == 128) { ERGM_GEMM_LAYOUTS(128, 128) }
-    else { ERGM_GEMM_LAYOUTS(64, 64) }
-#undef ERGM_GEMM_LAYOUTS
+    if (al == ERGM_MK && bl == ERGM_NK) launch_any<false, false, EPI, OB>(a, p, s);
+    else if (al == ERGM_MK && bl == ERGM_KN) launch_any<false, true, EPI, OB>(a, p, s);
+    else if (al == ERGM_KM && bl == ERGM_NK) launch_any<true, false, EPI, OB>(a, p, s);
+    else launch_any<true, true, EPI, OB>(a, p, s);
 }
 
 template <int EPI, bool OB>
@@ -580,6 +655,13 @@ static void launch_reduce(const GemmArgs& a, int split, hipStream_t s) {
 }  // namespace ergm
 
 using namespace ergm;
+
+extern "C" int ergm_gemm_tune(int cfg, int split) {
+    ERGM_CHECK_ARG(cfg >= -1 && cfg < kNumCfgs && split >= 0, "gemm_tune: cfg in [-1, %d), split >= 0", kNumCfgs);
+    g_force_cfg = cfg;
+    g_force_split = split;
+    return ERGM_OK;
+}
 
 extern "C" size_t ergm_gemm_workspace_size(const ergm_gemm_desc* d) {
     if (!d) return 0;

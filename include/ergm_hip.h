@@ -88,6 +88,10 @@ typedef struct {
     const float* alpha_dev;  /* optional device scalar multiplied into alpha (autograd grad_output) */
 } ergm_gemm_desc;
 
+/* Tuning hook (calling thread only): force pipelined-kernel configuration `cfg` (tile / wave grid /
+ * LDS stages, see kCfgs in ergm_amd/csrc/gemm.hip) and split-K count for later ergm_gemm calls;
+ * cfg = -1 restores the automatic choice.  Used by tools/gemm_tune.py.                          */
+int ergm_gemm_tune(int cfg, int split);
 /* Workspace bytes ergm_gemm needs for `desc` (split-K partial slabs); 0 if none. */
 size_t ergm_gemm_workspace_size(const ergm_gemm_desc* desc);
 int ergm_gemm(const ergm_gemm_desc* desc, const void* A, const void* B, void* C, void* workspace,
