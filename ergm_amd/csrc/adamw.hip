@@ -9,34 +9,63 @@
 
 namespace ergm {
 
+__device__ __forceinline__ void adamw_one(float4& pp, const float4& gg, float4& mm, float4& vv, bf16x4& ob, float decay,
+                                          float one_m_b1, float b2, float one_m_b2, float eps, float step_size,
+                                          float bc2_sqrt) {
+    float* P = reinterpret_cast<float*>(&pp);
+    const float* G = reinterpret_cast<const float*>(&gg);
+    float* Mv = reinterpret_cast<float*>(&mm);
+    float* Vv = reinterpret_cast<float*>(&vv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float x = P[j] * decay;
+        float mj = Mv[j] + one_m_b1 * (G[j] - Mv[j]);
+        float vj = Vv[j] * b2 + one_m_b2 * (G[j] * G[j]);
+        float denom = sqrtf(vj) / bc2_sqrt + eps;
+        x = x + (-step_size) * (mj / denom);
+        P[j] = x;
+        Mv[j] = mj;
+        Vv[j] = vj;
+        ob[j] = f2bf(x);
+    }
+}
+
+__device__ __forceinline__ float4 nt_load4(const float4* p) {  // gradients are read exactly once
+    f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(t[0], t[1], t[2], t[3]);
+}
+
+// Two float4 groups per thread per iteration (8 independent 16-B loads in flight before any math).
 __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                     float4* __restrict__ m, float4* __restrict__ v,
                                                     bf16x4* __restrict__ pb, size_t n4, float decay, float one_m_b1,
                                                     float b2, float one_m_b2, float eps, float step_size,
                                                     float bc2_sqrt) {
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-        float* P = reinterpret_cast<float*>(&pp);
-        float* G = reinterpret_cast<float*>(&gg);
-        float* Mv = reinterpret_cast<float*>(&mm);
-        float* Vv = reinterpret_cast<float*>(&vv);
-        bf16x4 ob;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float x = P[j] * decay;
-            float mj = Mv[j] + one_m_b1 * (G[j] - Mv[j]);
-            float vj = Vv[j] * b2 + one_m_b2 * (G[j] * G[j]);
-            float denom = sqrtf(vj) / bc2_sqrt + eps;
-            x = x + (-step_size) * (mj / denom);
-            P[j] = x;
-            Mv[j] = mj;
-            Vv[j] = vj;
-            ob[j] = f2bf(x);
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += 2 * stride) {
+        const size_t i2 = i + stride;
+        const bool two = i2 < n4;
+        float4 p0 = p[i], g0 = nt_load4(g + i), m0 = m[i], v0 = v[i];
+        float4 p1, g1, m1, v1;
+        if (two) {
+            p1 = p[i2];
+            g1 = nt_load4(g + i2);
+            m1 = m[i2];
+            v1 = v[i2];
         }
-        p[i] = pp;
-        m[i] = mm;
-        v[i] = vv;
-        if (pb) pb[i] = ob;
+        bf16x4 o0, o1;
+        adamw_one(p0, g0, m0, v0, o0, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+        p[i] = p0;
+        m[i] = m0;
+        v[i] = v0;
+        if (pb) pb[i] = o0;
+        if (two) {
+            adamw_one(p1, g1, m1, v1, o1, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+            p[i2] = p1;
+            m[i2] = m1;
+            v[i2] = v1;
+            if (pb) pb[i2] = o1;
+        }
     }
 }
 
@@ -64,6 +93,11 @@ static unsigned grid_for(size_t n4) {
     return (unsigned)(blocks < 8192 ? (blocks ? blocks : 1) : 8192);
 }
 
+static unsigned grid_for2(size_t n4) {  // adamw: each thread covers two strided float4 groups
+    size_t blocks = (n4 + 511) / 512;
+    return (unsigned)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
+}
+
 }  // namespace ergm
 
 using namespace ergm;
@@ -81,7 +115,7 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     float decay = (float)(1.0 - (double)lr * (double)weight_decay);
     float one_m_b1 = (float)(1.0 - (double)beta1);
     float one_m_b2 = (float)(1.0 - (double)beta2);
-    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for2(n4)), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2, one_m_b2, eps, step_size,
                        bc2_sqrt);
     return check_launch("adamw");

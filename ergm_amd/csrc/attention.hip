@@ -223,7 +223,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
     const float* lse = a.lse + ((size_t)b * a.H + h) * a.Sq;
-    const float* dl = a.delta + ((size_t)b * a.H + h) * a.Sq;
 
     // Kᵀ / Vᵀ as B operands: lane l needs K[key][32ks + 8g + j]
     bf16x8 kf[2], vf[2];
@@ -245,10 +244,27 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
         __syncthreads();
         stage_tile(sQ, Qb, a.ldq, q0, a.Sq, 0);
         stage_tile(sdO, dOb, a.lddo, q0, a.Sq, 0);
-        if (threadIdx.x < AT_T) {
-            int qq = q0 + threadIdx.x;
-            sL[threadIdx.x] = qq < a.Sq ? lse[qq] : 0.f;
-            sD[threadIdx.x] = qq < a.Sq ? dl[qq] : 0.f;
+        {   // delta[q] = Σ_d dO[q,d]·O[q,d] for the tile's 64 queries: 4 threads per query row
+            const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
+            const int qq = q0 + ql;
+            float dsum = 0.f;
+            if (qq < a.Sq) {
+                const __bf16* od = a.o + ((size_t)b * a.Sq + qq) * a.ldo + h * AT_D + part * 16;
+                const __bf16* dd = dOb + (size_t)qq * a.lddo + part * 16;
+#pragma unroll
+                for (int c = 0; c < 16; c += 8) {
+                    bf16x8 x = *reinterpret_cast<const bf16x8*>(dd + c);
+                    bf16x8 y = *reinterpret_cast<const bf16x8*>(od + c);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) dsum += bf2f(x[j]) * bf2f(y[j]);
+                }
+            }
+            dsum += __shfl_xor(dsum, 1, 64);
+            dsum += __shfl_xor(dsum, 2, 64);
+            if (part == 0) {
+                sL[ql] = qq < a.Sq ? lse[qq] : 0.f;
+                sD[ql] = dsum;
+            }
         }
         __syncthreads();
         f32x4 p[4], ds[4];
@@ -314,7 +330,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
     const size_t sidx = ((size_t)b * a.H + h) * a.Sq + q;
     const float lq = q < a.Sq ? a.lse[sidx] : 0.f;
-    const float dq_delta = q < a.Sq ? a.delta[sidx] : 0.f;
+    float dq_delta = 0.f;  // Σ_d dO[q,d]·O[q,d]: the 4 lane groups sharing query q each sum 16 dims
+    if (q < a.Sq) {
+        const __bf16* od = a.o + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D + g * 16;
+        const __bf16* dd = dOb + (size_t)q * a.lddo + g * 16;
+#pragma unroll
+        for (int c = 0; c < 16; c += 8) {
+            bf16x8 x = *reinterpret_cast<const bf16x8*>(dd + c);
+            bf16x8 y = *reinterpret_cast<const bf16x8*>(od + c);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dq_delta += bf2f(x[j]) * bf2f(y[j]);
+        }
+    }
+    dq_delta += __shfl_xor(dq_delta, 16, 64);
+    dq_delta += __shfl_xor(dq_delta, 32, 64);
 
     bf16x8 qf[2], dof[2];
     qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
@@ -423,8 +452,6 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
     a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
     a.scale = 0.125f;
     hipStream_t s = as_stream(stream);
-    size_t n = (size_t)B * Sq * H;
-    hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
     if (causal) {
         hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, gk, dim3(256), 0, s, a);

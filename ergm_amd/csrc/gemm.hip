@@ -533,18 +533,21 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
         p.cfg = g_force_cfg;
         split = std::max(1, g_force_split);
     } else {
-        // Tile choice per shape class (measured on MI355X, tools/gemm_tune.py): large outputs take
-        // big 8-wave tiles; the T x E projections take 64x64 / 128x64 tiles; deep K splits.
-        const long t128 = tiles_of(M, N, 128, 128), t64 = tiles_of(M, N, 64, 64);
-        if (t128 >= 240) {
-            p.cfg = 1;
-        } else if (K >= 4096 && d->split_k != 1) {
-            p.cfg = 1;
-            split = std::max(1, std::min((int)((512 + t128 - 1) / t128), K / 1024));
+        // Tile choice per shape class, from tools/gemm_tune.py on MI355X (gpurun_out/gemm_tune.json,
+        // summarized in DESIGN.md): the 256x256 8-wave tile for the vocabulary-wide LM head, 8-wave
+        // 128x128 (32x64 per wave, 2 stages) for mid/large activation GEMMs, 4-wave 128x128 for large
+        // weight gradients (A = activations^T), deep K split 4 ways, 64x64 without split otherwise
+        // (split-K's extra reduce launch cost more than it saved at these sizes).
+        const long t128 = tiles_of(M, N, 128, 128);
+        if (K >= 4096 && t128 < 240 && d->split_k != 1) {
+            p.cfg = 2;
+            split = std::max(1, std::min(4, K / 1024));
+        } else if (t128 >= 4000) {
+            p.cfg = 6;
+        } else if (t128 >= 140) {
+            p.cfg = d->a_layout == ERGM_KM ? 2 : 10;
         } else {
             p.cfg = 0;
-            if (t64 < 200 && K >= 1024 && d->split_k != 1)
-                split = std::max(1, std::min((int)((400 + t64 - 1) / t64), K / 512));
         }
     }
     if (p.cfg >= 0) {
