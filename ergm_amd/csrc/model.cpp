@@ -57,9 +57,17 @@ struct ergm_model_plan {
     int* n_valid_local;
     // backward scratch
     float *dh, *dy, *dcap, *delta;
-    __bf16 *dh_b, *d_o, *dqkv, *dxq, *dkv_all, *dpre;
-    char* scratch;
+    __bf16 *d_o, *dkv_all;
+    // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
+    // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
+    std::vector<__bf16*> dhb, dpre, dxq, dqkv;
+    char *scratch, *scratch2;
     size_t scratch_bytes;
+    // Two HIP streams: the caller's stream runs the critical chain; `side` runs weight-gradient GEMMs
+    // (and the stacked caption K/V GEMM in forward), forked/joined with events.
+    hipStream_t side;
+    hipEvent_t ev_fork;
+    std::vector<hipEvent_t> ev_join;  // one per backward stage (L layers + head + embed)
     // inputs
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
     const float *vis, *aud;
@@ -121,10 +129,16 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->n_valid_local = c.take<int>(4);
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
-    P->dh_b = c.take<__bf16>(T * E); P->d_o = c.take<__bf16>(T * E);
-    P->dqkv = c.take<__bf16>(T * 3 * E); P->dxq = c.take<__bf16>(T * E);
+    P->d_o = c.take<__bf16>(T * E);
     P->dkv_all = c.take<__bf16>(T * 2 * E * L);
-    P->dpre = c.take<__bf16>(T * F);
+    P->dhb.assign(3 * L + 1, nullptr);
+    for (size_t i = 0; i < 3 * L + 1; ++i) P->dhb[i] = c.take<__bf16>(T * E);
+    P->dpre.assign(L, nullptr); P->dxq.assign(L, nullptr); P->dqkv.assign(L, nullptr);
+    for (size_t l = 0; l < L; ++l) {
+        P->dpre[l] = c.take<__bf16>(T * F);
+        P->dxq[l] = c.take<__bf16>(T * E);
+        P->dqkv[l] = c.take<__bf16>(T * 3 * E);
+    }
     P->scratch = c.take<char>(0);
     P->resid = P->resid_v.data();
     return c.off;
@@ -151,21 +165,43 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
-    return ergm_gemm(&g, A, B, C, P->scratch, P->scratch_bytes, s);
+    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : P->scratch;
+    return ergm_gemm(&g, A, B, C, ws, P->scratch_bytes, s);
 }
 
 int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, int cols, int ldx, float* out) {
     ERGM_TRY(ws_need(P, ergm_colsum_workspace_size(rows, cols)));
     if (P->dry) return ERGM_OK;
-    return ergm_colsum(X, dt, rows, cols, ldx, out, 0, P->scratch, P->scratch_bytes, s);
+    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : P->scratch;
+    return ergm_colsum(X, dt, rows, cols, ldx, out, 0, ws, P->scratch_bytes, s);
 }
 
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]).
 // With fused_bias the A operand's column M is all ones and gB == gW + M·N, so one GEMM over M+1
 // rows writes [gW; gB]; otherwise the bias gradient is a separate column sum of dY.
-int dw_gemm(ergm_model_plan* P, hipStream_t s, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
+// Make the side stream wait for everything issued so far on `s` (the producer of a dW GEMM's dY).
+int fork_side(ergm_model_plan* P, hipStream_t s) {
+    if (P->dry) return ERGM_OK;
+    if (hipEventRecord(P->ev_fork, s) != hipSuccess || hipStreamWaitEvent(P->side, P->ev_fork, 0) != hipSuccess)
+        return fail(ERGM_EHIP, "model: stream fork failed");
+    return ERGM_OK;
+}
+
+// Record stage event `k` on the side stream / make `s` wait for a recorded stage event.
+int side_mark(ergm_model_plan* P, int k) {
+    if (P->dry) return ERGM_OK;
+    return hipEventRecord(P->ev_join[k], P->side) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: event record");
+}
+int join_side(ergm_model_plan* P, hipStream_t s, int k) {
+    if (P->dry) return ERGM_OK;
+    return hipStreamWaitEvent(s, P->ev_join[k], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: stream join");
+}
+
+int dw_gemm(ergm_model_plan* P, hipStream_t s_main, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB) {
     const int T = P->T;
+    ERGM_TRY(fork_side(P, s_main));
+    hipStream_t s = P->dry ? s_main : P->side;
     if (P->fused_bias)
         return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
     ERGM_TRY(gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE));
@@ -173,11 +209,11 @@ int dw_gemm(ergm_model_plan* P, hipStream_t s, int M, int N, const __bf16* A, in
 }
 
 int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
-           float* dgamma, float* dbeta) {
+           float* dgamma, float* dbeta, __bf16* dh_b) {
     const int T = P->T, E = P->d.n_embd;
     ERGM_TRY(ws_need(P, ergm_layernorm_bwd_workspace_size(T, E)));
     if (P->dry) return ERGM_OK;
-    return ergm_layernorm_bwd(P->dy, x, mean, rstd, gamma, P->dh, P->dh_b, dgamma, dbeta, P->scratch, P->scratch_bytes,
+    return ergm_layernorm_bwd(P->dy, x, mean, rstd, gamma, P->dh, dh_b, dgamma, dbeta, P->scratch, P->scratch_bytes,
                               T, E, s);
 }
 
@@ -227,7 +263,7 @@ extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     do_backward_head(&P, nullptr, nullptr);
     do_backward_layer(&P, 0, nullptr);
     do_backward_embed(&P, nullptr);
-    return ((act + 255) & ~(size_t)255) + P.need + 256;
+    return ((act + 255) & ~(size_t)255) + 2 * (((P.need + 255) & ~(size_t)255) + 256);
 }
 
 extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* ws,
@@ -252,8 +288,19 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->L2E = 2 * d.n_embd * d.n_layer;
     size_t act = carve(P, reinterpret_cast<char*>(ws));
     act = (act + 255) & ~(size_t)255;
+    P->scratch_bytes = (ws_bytes - act) / 2 & ~(size_t)255;
     P->scratch = reinterpret_cast<char*>(ws) + act;
-    P->scratch_bytes = ws_bytes - act;
+    P->scratch2 = P->scratch + P->scratch_bytes;
+    P->side = nullptr;
+    P->ev_fork = nullptr;
+    P->ev_join.assign(d.n_layer + 3, nullptr);
+    bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming) == hipSuccess;
+    for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        ergm_model_destroy(P);
+        return fail(ERGM_EHIP, "model_create: stream/event creation failed");
+    }
     P->dry = false;
     P->need = 0;
     P->have_fwd = false;
@@ -278,7 +325,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
         if (rc == ERGM_OK) rc = fill_ones_col(P->cap, P->T, P->XE, d.n_embd, nullptr);
         if (rc == ERGM_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = fail(ERGM_EHIP, "model_create: sync");
         if (rc != ERGM_OK) {
-            delete P;
+            ergm_model_destroy(P);
             return rc;
         }
     }
@@ -293,6 +340,12 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
 }
 
 extern "C" int ergm_model_destroy(ergm_model_plan* P) {
+    if (!P) return ERGM_OK;
+    if (P->side) hipStreamSynchronize(P->side);
+    for (auto e : P->ev_join)
+        if (e) hipEventDestroy(e);
+    if (P->ev_fork) hipEventDestroy(P->ev_fork);
+    if (P->side) hipStreamDestroy(P->side);
     delete P;
     return ERGM_OK;
 }
@@ -330,11 +383,15 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     if (!P->dry)
         ERGM_TRY(embed_fwd_ld(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap,
                               P->XE, B, S, E, d.vocab, s));
-    // all L cross-attention K/V projections of the caption embeddings in one GEMM
+    // all L cross-attention K/V projections of the caption embeddings in one GEMM, on the side stream
+    // (it overlaps block 0's self-attention; joined before block 0's cross-attention)
     {
-    Probe pr(P, 4, s);
-    ERGM_TRY(gemm(P, s, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
-                  ERGM_EPI_BIAS, p.capkv_b));
+        ERGM_TRY(fork_side(P, s));
+        hipStream_t ss = P->dry ? s : P->side;
+        Probe pr(P, 4, ss);
+        ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
+                      ERGM_EPI_BIAS, p.capkv_b));
+        ERGM_TRY(side_mark(P, L));
     }
     for (int l = 0; l < L; ++l) {
         LayerActs& a = P->la[l];
@@ -360,6 +417,7 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
                       ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
+        if (l == 0) ERGM_TRY(join_side(P, s, L));
         if (!P->dry)
             ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, P->XE, 0, s));
         ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
@@ -415,17 +473,22 @@ namespace {
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const ergm_model_params& p = P->p;
-    const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad;
-    // dh_f = dlogits · wte  (contraction over the padded vocab), dwte = dlogitsᵀ · ln_f(h)
+    const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad, L = d.n_layer;
+    // dh_f = dlogits · wte (contraction over the padded vocab) on the main chain; the tied-weight
+    // gradient dwte = dlogitsᵀ · ln_f(h) on the side stream (joined before the embedding backward adds
+    // the lookup gradients into the same buffer).
     {
         Probe pr(P, 2, s);
         ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
                       nullptr, nullptr, 0, nullptr, 0, gscale));
     }
     {
-        Probe pr(P, 3, s);
-        ERGM_TRY(gemm(P, s, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
+        ERGM_TRY(fork_side(P, s));
+        hipStream_t ss = P->dry ? s : P->side;
+        Probe pr(P, 3, ss);
+        ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
                       ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, gscale));
+        ERGM_TRY(side_mark(P, L + 1));
     }
     if (P->dry) return ERGM_OK;
     if (P->emo_labels) {
@@ -435,61 +498,77 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
         if (hipMemsetAsync(p.g_emo_w, 0, (size_t)7 * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
     }
     if (hipMemsetAsync(P->dh, 0, (size_t)T * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
-    return ln_bwd(P, s, P->resid[3 * d.n_layer], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b);
+    return ln_bwd(P, s, P->resid[3 * L], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b, P->dhb[3 * L]);
 }
 
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const int T = P->T, E = d.n_embd, F = d.n_inner, H = d.n_head, B = d.batch, S = d.seq, L2E = P->L2E;
+    const int L = d.n_layer;
     LayerActs a = P->dry ? LayerActs{} : P->la[l];
     const float* x0 = P->dry ? nullptr : P->resid[3 * l];
     const float* x1 = P->dry ? nullptr : P->resid[3 * l + 1];
     const float* x2 = P->dry ? nullptr : P->resid[3 * l + 2];
+    __bf16* dh3 = P->dhb[3 * l + 3];  // bf16 grad of this block's output (written by the previous stage)
+    __bf16* dh2 = P->dhb[3 * l + 2];
+    __bf16* dh1 = P->dhb[3 * l + 1];
+    __bf16* dh0 = P->dhb[3 * l];
+    __bf16* dpre = P->dpre[l];
+    __bf16* dxq = P->dxq[l];
+    __bf16* dqkv = P->dqkv[l];
     // ---- MLP: x3 = x2 + gelu(ln2(x2)·Wfc + bfc)·Wm + bm
-    ERGM_TRY(dw_gemm(P, s, F, E, a.act, P->XF, P->dh_b, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
-    ERGM_TRY(gemm(P, s, T, F, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK, P->dpre, F, ERGM_BF16,
+    ERGM_TRY(dw_gemm(P, s, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
+    ERGM_TRY(gemm(P, s, T, F, E, dh3, E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK, dpre, F, ERGM_BF16,
                   ERGM_EPI_GELU_BWD, nullptr, a.pre, F));
-    ERGM_TRY(dw_gemm(P, s, E, F, a.ln2, P->XE, P->dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
-    ERGM_TRY(gemm(P, s, T, E, F, P->dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
+    ERGM_TRY(dw_gemm(P, s, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
+    ERGM_TRY(gemm(P, s, T, E, F, dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
+    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B), dh2));
     // ---- cross-attention: x2 = x1 + Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp
-    ERGM_TRY(dw_gemm(P, s, E, E, a.xo, P->XE, P->dh_b, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
+    ERGM_TRY(dw_gemm(P, s, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, dh2, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
                   ERGM_EPI_NONE));
     if (!P->dry) {
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
         __bf16* dkl = P->dkv_all + (size_t)l * 2 * E;
-        ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, P->dxq, dkl, dkl + E, B, H, S, S, E,
+        ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, dxq, dkl, dkl + E, B, H, S, S, E,
                                L2E, L2E, P->XE, E, E, L2E, L2E, 0, s));
     }
-    ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, P->dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, P->dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
+    ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
+    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B), dh1));
     // ---- self-attention: x1 = x0 + Attn(ln_1(x0)·Wqkv + b)·Wap + bap
-    ERGM_TRY(dw_gemm(P, s, E, E, a.ao, P->XE, P->dh_b, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, P->dh_b, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
+    ERGM_TRY(dw_gemm(P, s, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
+    ERGM_TRY(gemm(P, s, T, E, E, dh1, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
                   ERGM_EPI_NONE));
     if (!P->dry) {
-        ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, P->dqkv, P->dqkv + E,
-                               P->dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, s));
+        ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, dqkv, dqkv + E,
+                               dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, s));
     }
-    ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, P->dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
-    ERGM_TRY(gemm(P, s, T, E, 3 * E, P->dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
+    ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
+    ERGM_TRY(gemm(P, s, T, E, 3 * E, dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
                   ERGM_F32, ERGM_EPI_NONE));
-    return ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B));
+    ERGM_TRY(ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B), dh0));
+    // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
+    // those of the block differentiated before, so block l+1's gradients are final on return.
+    ERGM_TRY(side_mark(P, l));
+    if (l + 1 < L) ERGM_TRY(join_side(P, s, l + 1));
+    return ERGM_OK;
 }
 
 int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const ergm_model_params& p = P->p;
-    const int T = P->T, E = d.n_embd, L2E = P->L2E;
-    // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all, dcap = dKV_all·Wᵀ
+    const int T = P->T, E = d.n_embd, L2E = P->L2E, L = d.n_layer;
+    // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
     ERGM_TRY(dw_gemm(P, s, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
+    ERGM_TRY(side_mark(P, L + 2));
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));
     if (P->dry) return ERGM_OK;
+    // every side-stream gradient (incl. the LM-head dwte) is final before the lookup gradients are added
+    ERGM_TRY(join_side(P, s, L + 2));
     return ergm_embed_bwd(P->ids, P->tt, P->cap_ids, P->dh, P->dcap, p.g_wte, p.g_wpe, P->scratch, P->scratch_bytes,
                           d.batch, d.seq, E, d.vocab, s);
 }

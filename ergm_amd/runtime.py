@@ -115,9 +115,12 @@ class ModelRunner:
         self.dp.begin()
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
         Lyr = self.layout.L
+        # bucket i = (head +) block L-1-i; its weight gradients are joined one stage later (ergm_hip.h)
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
-            self.dp.bucket_ready(i, self.grad)
+            if i >= 1:
+                self.dp.bucket_ready(i - 1, self.grad)
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
+        self.dp.bucket_ready(Lyr - 1, self.grad)
         self.dp.bucket_ready(Lyr, self.grad)
         self.dp.finish(self.grad)

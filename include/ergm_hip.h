@@ -232,7 +232,10 @@ int ergm_model_forward(ergm_model_plan* plan, void* logits, float* emo_logits, f
 /* Backward in stages so a DP caller can overlap communication:
  *   ergm_model_backward_head  — LM head + emotion head + ln_f (grads of wte(part), emo, ln_f)
  *   ergm_model_backward_layer — block `layer` (call for L-1 … 0)
- *   ergm_model_backward_embed — stacked caption K/V projection + embeddings (wte rest, wpe)   */
+ *   ergm_model_backward_embed — stacked caption K/V projection + embeddings (wte rest, wpe)
+ * Weight-gradient GEMMs run on the plan's internal side stream.  Ordering guarantee on `stream`:
+ * after backward_layer(l) the gradients of the head stage and of blocks > l are final (block l's
+ * own weight gradients are joined by the NEXT stage); after backward_embed every gradient is. */
 int ergm_model_backward_head(ergm_model_plan* plan, const float* grad_scale_dev, void* stream);
 int ergm_model_backward_layer(ergm_model_plan* plan, int layer, void* stream);
 int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
