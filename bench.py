@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap-optim", action="store_true",
+                    help="apply AdamW in opt.step() instead of per gradient bucket during backward")
     ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
     args = ap.parse_args()
 
@@ -102,7 +104,7 @@ def main():
     cfg = gpt2_small()
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
-    opt = FusedAdamW([model.flat], lr=2e-5, model=model)
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
     total = args.warmup + args.steps
     sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=int(0.1 * total),
                                                       num_training_steps=total, power=2)
@@ -163,7 +165,7 @@ def main():
     V, E = cfg.vocab_size, cfg.n_embd
     probe_flops = {1: 2.0 * T * V * E, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
                    4: 2.0 * T * E * (2 * E * cfg.n_layer)}[args.probe]
-    probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (gemm_kernel<128,128,MK,NK,none,bf16>)",
+    probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
                   2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
     achieved = probe_flops / (probe_ms * 1e-3) / 1e12
     step_flops = flops_per_utterance(S) * B
@@ -190,6 +192,8 @@ def main():
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S), 0)},
+        "optimizer": "FusedAdamW " + ("per-bucket, overlapped with backward" if not args.no_overlap_optim
+                                      else "after backward"),
         "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
                           "emotion_acc": round(correct.item() / (B * total), 4)},
     }

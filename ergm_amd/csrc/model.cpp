@@ -26,6 +26,11 @@ namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
                      int rows, int E, float eps, hipStream_t s);
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
+int ln_bwd_nparts(int rows);
+int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
+                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s);
+int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
+                           hipStream_t s);
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
                  int V, hipStream_t s);
@@ -61,6 +66,9 @@ struct ergm_model_plan {
     // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
     // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
     std::vector<__bf16*> dhb, dpre, dxq, dqkv;
+    // dγ/dβ partials of each LayerNorm backward (one slot per LN, reduced on the side stream)
+    std::vector<float*> ln_part;
+    int ln_slot;
     char *scratch, *scratch2;
     size_t scratch_bytes;
     // Two HIP streams: the caller's stream runs the critical chain; `side` runs weight-gradient GEMMs
@@ -133,6 +141,8 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->dkv_all = c.take<__bf16>(T * 2 * E * L);
     P->dhb.assign(3 * L + 1, nullptr);
     for (size_t i = 0; i < 3 * L + 1; ++i) P->dhb[i] = c.take<__bf16>(T * E);
+    P->ln_part.assign(3 * L + 1, nullptr);
+    for (size_t i = 0; i < 3 * L + 1; ++i) P->ln_part[i] = c.take<float>((size_t)2 * ln_bwd_nparts((int)T) * E);
     P->dpre.assign(L, nullptr); P->dxq.assign(L, nullptr); P->dqkv.assign(L, nullptr);
     for (size_t l = 0; l < L; ++l) {
         P->dpre[l] = c.take<__bf16>(T * F);
@@ -208,13 +218,17 @@ int dw_gemm(ergm_model_plan* P, hipStream_t s_main, int M, int N, const __bf16* 
     return colsum(P, s, dY, ERGM_BF16, T, N, ldy, gB);
 }
 
+// LayerNorm backward on the critical chain; its dγ/dβ partial reduction is forked to the side stream
+// (partials live in a per-LN slot, so nothing later overwrites them before the reduce runs).
 int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
-           float* dgamma, float* dbeta, __bf16* dh_b) {
-    const int T = P->T, E = P->d.n_embd;
-    ERGM_TRY(ws_need(P, ergm_layernorm_bwd_workspace_size(T, E)));
+           float* dgamma, float* dbeta, __bf16* dh_b, int slot) {
     if (P->dry) return ERGM_OK;
-    return ergm_layernorm_bwd(P->dy, x, mean, rstd, gamma, P->dh, dh_b, dgamma, dbeta, P->scratch, P->scratch_bytes,
-                              T, E, s);
+    const int T = P->T, E = P->d.n_embd;
+    float* pg = P->ln_part[slot];
+    float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
+    ERGM_TRY(layernorm_bwd_main(P->dy, x, mean, rstd, gamma, P->dh, dh_b, pg, pb, T, E, s));
+    ERGM_TRY(fork_side(P, s));
+    return layernorm_param_reduce(pg, pb, T, E, dgamma, dbeta, P->side);
 }
 
 struct Probe {  // records the probe events around one launch when `id` is the active probe
@@ -498,7 +512,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
         if (hipMemsetAsync(p.g_emo_w, 0, (size_t)7 * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
     }
     if (hipMemsetAsync(P->dh, 0, (size_t)T * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
-    return ln_bwd(P, s, P->resid[3 * L], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b, P->dhb[3 * L]);
+    return ln_bwd(P, s, P->resid[3 * L], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b, P->dhb[3 * L], 3 * L);
 }
 
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
@@ -523,7 +537,8 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, s, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
     ERGM_TRY(gemm(P, s, T, E, F, dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B), dh2));
+    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B), dh2,
+                    3 * l + 2));
     // ---- cross-attention: x2 = x1 + Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp
     ERGM_TRY(dw_gemm(P, s, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, dh2, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
@@ -537,7 +552,8 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
                   ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B), dh1));
+    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B), dh1,
+                    3 * l + 1));
     // ---- self-attention: x1 = x0 + Attn(ln_1(x0)·Wqkv + b)·Wap + bap
     ERGM_TRY(dw_gemm(P, s, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, dh1, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
@@ -549,7 +565,8 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
     ERGM_TRY(gemm(P, s, T, E, 3 * E, dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
                   ERGM_F32, ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B), dh0));
+    ERGM_TRY(ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B), dh0,
+                    3 * l));
     // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
     // those of the block differentiated before, so block l+1's gradients are final on return.
     ERGM_TRY(side_mark(P, l));

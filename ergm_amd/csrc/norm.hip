@@ -298,26 +298,46 @@ extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {
     return 2 * (size_t)nb * E * sizeof(float);
 }
 
+namespace ergm {
+// Main LayerNorm-backward pass only: dres += dx, dres_bf16, and per-block dγ/dβ partials
+// (part_g/part_b: ln_bwd_nparts(rows) x E floats each), reduced later by layernorm_param_reduce.
+int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
+
+int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
+                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s) {
+    ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
+    ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
+    const int nb = ln_bwd_nparts(rows);
+    auto* db = reinterpret_cast<__bf16*>(dres_bf16);
+    switch (cdiv(E, 256)) {
+        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+    }
+    return check_launch("layernorm_bwd");
+}
+
+int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
+                           hipStream_t s) {
+    ERGM_CHECK_ARG(part_g && part_b && dgamma && dbeta, "layernorm_param_reduce: null argument");
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2), dim3(256), 0, s, part_g, part_b,
+                       ln_bwd_nparts(rows), E, dgamma, dbeta);
+    return check_launch("layernorm_param_reduce");
+}
+}  // namespace ergm
+
 extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
                                   const float* gamma, float* dres, void* dres_bf16, float* dgamma, float* dbeta,
                                   void* ws, size_t ws_bytes, int rows, int E, void* stream) {
-    ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && dgamma && dbeta, "layernorm_bwd: null argument");
-    ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
+    ERGM_CHECK_ARG(dgamma && dbeta, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(ws && ws_bytes >= ergm_layernorm_bwd_workspace_size(rows, E), "layernorm_bwd: workspace too small");
-    int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
+    const int nb = ln_bwd_nparts(rows);
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
     hipStream_t s = as_stream(stream);
-    auto* db = reinterpret_cast<__bf16*>(dres_bf16);
-    int nv = cdiv(E, 256);
-    switch (nv) {
-        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
-        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
-        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
-        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, pg, pb, rows, E); break;
-    }
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2), dim3(256), 0, s, pg, pb, nb, E, dgamma, dbeta);
-    return check_launch("layernorm_bwd");
+    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s));
+    return layernorm_param_reduce(pg, pb, rows, E, dgamma, dbeta, s);
 }
 
 extern "C" size_t ergm_colsum_workspace_size(int rows, int cols) { return colsum_ws(rows, cols); }

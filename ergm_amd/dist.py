@@ -52,23 +52,44 @@ class DPSync:
     def begin(self) -> None:
         self._works = []
 
-    def bucket_ready(self, k: int, grad: torch.Tensor) -> None:
-        """Start the all-reduce of bucket k of the flat gradient buffer `grad`."""
-        if not self.active:
+    def _side(self, dev):
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        return self._stream
+
+    def bucket_ready(self, k: int, grad: torch.Tensor, post=None) -> None:
+        """Bucket k of the flat gradient buffer `grad` is final on the current stream: start its
+        all-reduce (SUM) on the side stream, then run ``post(a, b)`` there once the reduced values are
+        in place (the overlapped optimizer update of that parameter range)."""
+        if not self.active and post is None:
             return
-        import torch.distributed as dist
         a, b = self.buckets[k]
         if grad.is_cuda:
             cur = torch.cuda.current_stream(grad.device)
-            if self._stream is None:
-                self._stream = torch.cuda.Stream(grad.device)
+            side = self._side(grad.device)
             ev = torch.cuda.Event()
             ev.record(cur)
-            with torch.cuda.stream(self._stream):
-                self._stream.wait_event(ev)
-                self._works.append(dist.all_reduce(grad[a:b], group=self.pg, async_op=True))
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                if self.active:
+                    import torch.distributed as dist
+                    work = dist.all_reduce(grad[a:b], group=self.pg, async_op=True)
+                    if post is not None:
+                        work.wait()  # side stream waits for the collective; no host synchronisation
+                    else:
+                        self._works.append(work)
+                if post is not None:
+                    post(a, b)
         else:
-            self._works.append(dist.all_reduce(grad[a:b], group=self.pg, async_op=True))
+            if self.active:
+                import torch.distributed as dist
+                work = dist.all_reduce(grad[a:b], group=self.pg, async_op=True)
+                if post is not None:
+                    work.wait()
+                else:
+                    self._works.append(work)
+            if post is not None:
+                post(a, b)
 
     def finish(self, grad: torch.Tensor) -> None:
         """Make the current stream wait for every outstanding bucket (no host synchronisation)."""

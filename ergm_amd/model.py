@@ -88,7 +88,11 @@ class _FusedTrainStep(torch.autograd.Function):
             gl = gl.reshape(-1)[2:3] if gl.numel() == 3 else gl.reshape(1)
             gl = gl.float().contiguous()
         if flat.grad is None:
-            runner.backward(gl)                      # writes model.grad_buf
+            post = None
+            opt = model._overlap_opt
+            if opt is not None:
+                post = opt._backward_hook(flat, model)   # per-bucket AdamW, overlapped with backward
+            runner.backward(gl, post)                # writes model.grad_buf
             flat.grad = model.grad_buf
         else:
             # accumulate semantics when the caller did not zero the gradient
@@ -122,6 +126,7 @@ class GPT2LMHeadModel(nn.Module):
         self._tmp = None
         self._runners: Dict[tuple, ModelRunner] = {}
         self._b16_version = -1
+        self._overlap_opt = None
         self.process_group = process_group
         self.init_weights()
 

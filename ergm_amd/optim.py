@@ -16,8 +16,20 @@ from . import ops
 
 
 class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW semantics as one HIP kernel over the flat parameter buffer.
+
+    ``overlap=True`` (needs ``model``): the update of each gradient bucket is launched during the
+    backward pass, on the side stream, as soon as that bucket is final (after its all-reduce under
+    data parallelism) — AdamW's 30 B/param of HBM traffic then overlaps the remaining backward
+    instead of following it.  It uses the learning rate in ``param_groups`` at backward time, which
+    is the one ``step()`` would use in the reference loop (zero_grad → backward → step → sched.step,
+    src/main.py:152-156, no gradient clipping in between), and ``step()`` only advances the step count.  Each backward applies one update, so this mode is for loops that
+    call ``backward()`` once per ``step()`` (the reference's); gradient accumulation (a backward onto
+    an existing ``.grad``) falls back to updating in ``step()``.
+    """
+
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 model=None):
+                 model=None, overlap: bool = False):
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         if not 0.0 <= eps:
@@ -26,6 +38,42 @@ class FusedAdamW(torch.optim.Optimizer):
             raise ValueError(f"Invalid beta parameters: {betas}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.model = model  # when given, its bf16 shadow is refreshed in the same pass
+        self._applied = set()
+        if overlap:
+            if model is None:
+                raise ValueError("overlap=True needs model=")
+            model._overlap_opt = self
+
+    def _state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    def _group_of(self, p):
+        for g in self.param_groups:
+            if any(q is p for q in g["params"]):
+                return g
+        return None
+
+    def _backward_hook(self, flat, model):
+        """Called by the model's backward: returns post(a, b) updating flat[a:b] from the gradient
+        buffer, or None when this optimizer does not own ``flat``."""
+        group = self._group_of(flat)
+        if group is None:
+            return None
+        st = self._state(flat)
+        t = int(st["step"].item()) + 1
+        b1, b2 = group["betas"]
+        m, v, g, shadow = st["exp_avg"], st["exp_avg_sq"], model.grad_buf, model.flat_b16
+        lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
+        self._applied.add(id(flat))
+
+        def post(a, b):
+            ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t)
+        return post
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -40,12 +88,13 @@ class FusedAdamW(torch.optim.Optimizer):
                     continue
                 if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
                     raise ValueError("FusedAdamW needs contiguous fp32 GPU parameters")
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st = self._state(p)
                 st["step"] += 1
+                if id(p) in self._applied:   # already updated bucket by bucket during backward
+                    self._applied.discard(id(p))
+                    if self.model is not None and p is self.model.flat:
+                        self.model._b16_version = p._version
+                    continue
                 t = int(st["step"].item())
                 shadow = None
                 if self.model is not None and p is self.model.flat:

@@ -107,7 +107,7 @@ class ModelRunner:
         return logits, emo, loss
 
     # ---- backward -----------------------------------------------------------------------
-    def backward(self, grad_scale: Optional[torch.Tensor]) -> None:
+    def backward(self, grad_scale: Optional[torch.Tensor], post=None) -> None:
         """Writes every parameter gradient into self.grad (overwrite, not accumulate).  With a
         process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final."""
         s = self._stream()
@@ -119,8 +119,8 @@ class ModelRunner:
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
             if i >= 1:
-                self.dp.bucket_ready(i - 1, self.grad)
+                self.dp.bucket_ready(i - 1, self.grad, post)
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
-        self.dp.bucket_ready(Lyr - 1, self.grad)
-        self.dp.bucket_ready(Lyr, self.grad)
+        self.dp.bucket_ready(Lyr - 1, self.grad, post)
+        self.dp.bucket_ready(Lyr, self.grad, post)
         self.dp.finish(self.grad)

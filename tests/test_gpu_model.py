@@ -137,6 +137,31 @@ def test_adamw_step_and_loss_decrease(gpu):
     assert losses[-1] < losses[0] - 0.05, losses
 
 
+def test_overlapped_adamw_matches_step_adamw(gpu):
+    """FusedAdamW(overlap=True) applies the same per-bucket update during backward: bitwise equal
+    parameters, moments and bf16 shadow to the plain step() path over a scheduled LR."""
+    from ergm_amd.optim import get_polynomial_decay_schedule_with_warmup
+    rec = _load("small_e128_v500.npz")
+    runs = []
+    for overlap in (False, True):
+        _, _, _, model, batch = _setup(rec, gpu)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=overlap)
+        sched = get_polynomial_decay_schedule_with_warmup(opt, 2, 10, power=2.0)
+        for _ in range(3):
+            opt.zero_grad()
+            out = _run(model, batch, gpu)
+            opt.step()
+            sched.step()
+        torch.cuda.synchronize()
+        st = opt.state[model.flat]
+        runs.append((model.flat.detach().clone(), model.flat_b16.clone(), st["exp_avg"].clone(),
+                     st["exp_avg_sq"].clone(), float(st["step"]), out.loss.item()))
+    a, b = runs
+    for x, y in zip(a[:4], b[:4]):
+        assert torch.equal(x, y)
+    assert a[4] == b[4] == 3.0 and a[5] == b[5]
+
+
 def test_backward_is_deterministic(gpu):
     rec = _load("small_e128_v500.npz")
     _, _, _, model, batch = _setup(rec, gpu)
