@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap-optim", action="store_true",
                     help="apply AdamW in opt.step() instead of per gradient bucket during backward")
+    ap.add_argument("--adamw-blocks", type=int, default=None,
+                    help="grid cap of the overlapped per-bucket AdamW (default: FusedAdamW.overlap_blocks)")
     ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
     args = ap.parse_args()
 
@@ -105,6 +107,8 @@ def main():
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
+    if args.adamw_blocks is not None:
+        opt.overlap_blocks = args.adamw_blocks
     total = args.warmup + args.steps
     sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=int(0.1 * total),
                                                       num_training_steps=total, power=2)
@@ -147,6 +151,7 @@ def main():
         e0, e1 = evs[i]
         _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
         step()
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (≈ dt when host-bound)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -192,8 +197,9 @@ def main():
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S), 0)},
-        "optimizer": "FusedAdamW " + ("per-bucket, overlapped with backward" if not args.no_overlap_optim
-                                      else "after backward"),
+        "optimizer": "FusedAdamW " + (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks})"
+                                      if not args.no_overlap_optim else "after backward"),
+        "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
         "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
                           "emotion_acc": round(correct.item() / (B * total), 4)},
     }

@@ -70,7 +70,7 @@ _SIGS = {
     "ergm_xent_fwd_bwd": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ergm_loss_finalize": (i32, [vp, i32, vp, vp, i32, vp, vp]),
-    "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, vp]),
+    "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
     "ergm_axpy": (i32, [vp, vp, sz, f32, vp]),
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
@@ -128,24 +128,47 @@ def check(rc: int, what: str) -> None:
     raise ErgmError(msg)
 
 
+def _hip():
+    if HipEvent._hip is None:
+        h = C.CDLL("libamdhip64.so")
+        h.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+        h.hipEventDestroy.argtypes = [C.c_void_p]
+        h.hipEventSynchronize.argtypes = [C.c_void_p]
+        h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+        h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+        h.hipStreamWaitEvent.argtypes = [C.c_void_p, C.c_void_p, C.c_uint]
+        HipEvent._hip = h
+    return HipEvent._hip
+
+
+HIP_EVENT_DISABLE_TIMING = 0x2
+HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000  # device-scope release: no L2 writeback at record time
+
+
 class HipEvent:
-    """A raw hipEvent_t (libamdhip64) for in-loop kernel timing by the native executor's probe."""
+    """A raw hipEvent_t (libamdhip64).  Default: a timing event for the executor's in-loop probe;
+    ``sync=True``: a device-scope ordering event between two streams of one device (no timing, no
+    system-scope fence, so recording it on the critical stream costs no cache writeback)."""
     _hip = None
 
-    def __init__(self):
-        if HipEvent._hip is None:
-            h = C.CDLL("libamdhip64.so")
-            h.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
-            h.hipEventDestroy.argtypes = [C.c_void_p]
-            h.hipEventSynchronize.argtypes = [C.c_void_p]
-            h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
-            HipEvent._hip = h
+    def __init__(self, sync: bool = False):
+        h = _hip()
+        flags = HIP_EVENT_DISABLE_SYSTEM_FENCE | (HIP_EVENT_DISABLE_TIMING if sync else 0)
         self.ev = C.c_void_p()
-        if HipEvent._hip.hipEventCreate(C.byref(self.ev)) != 0:
-            raise ErgmError("hipEventCreate failed")
+        if h.hipEventCreateWithFlags(C.byref(self.ev), flags) != 0:
+            raise ErgmError("hipEventCreateWithFlags failed")
+
+    def record(self, stream) -> None:
+        if _hip().hipEventRecord(self.ev, C.c_void_p(stream)) != 0:
+            raise ErgmError("hipEventRecord failed")
+
+    def wait(self, stream) -> None:
+        """Make `stream` (a hipStream_t as int) wait for the last record of this event."""
+        if _hip().hipStreamWaitEvent(C.c_void_p(stream), self.ev, 0) != 0:
+            raise ErgmError("hipStreamWaitEvent failed")
 
     def elapsed_ms(self, end: "HipEvent") -> float:
-        h = HipEvent._hip
+        h = _hip()
         if h.hipEventSynchronize(end.ev) != 0:
             raise ErgmError("hipEventSynchronize failed")
         ms = C.c_float()

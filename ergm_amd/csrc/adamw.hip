@@ -104,8 +104,9 @@ using namespace ergm;
 
 extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
                                float beta1, float beta2, float eps, float weight_decay, float step_size,
-                               float bc2_sqrt, void* stream) {
+                               float bc2_sqrt, int max_blocks, void* stream) {
     ERGM_CHECK_ARG(p && g && m && v, "adamw: null argument");
+    ERGM_CHECK_ARG(max_blocks >= 0, "adamw: max_blocks must be >= 0");
     ERGM_CHECK_ARG(n % 4 == 0, "adamw: n must be a multiple of 4");
     ERGM_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), "adamw: 16-byte alignment");
     ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw: bf16 copy alignment");
@@ -115,7 +116,9 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     float decay = (float)(1.0 - (double)lr * (double)weight_decay);
     float one_m_b1 = (float)(1.0 - (double)beta1);
     float one_m_b2 = (float)(1.0 - (double)beta2);
-    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for2(n4)), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+    unsigned grid = grid_for2(n4);
+    if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2, one_m_b2, eps, step_size,
                        bc2_sqrt);
     return check_launch("adamw");

@@ -189,6 +189,10 @@ int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, i
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]).
 // With fused_bias the A operand's column M is all ones and gB == gW + M·N, so one GEMM over M+1
 // rows writes [gW; gB]; otherwise the bias gradient is a separate column sum of dY.
+// Fork/join events order two streams of the same device: device-scope release is enough, and skipping
+// the system-scope fence avoids an L2 writeback at every record on the critical stream.
+constexpr unsigned kSyncEv = hipEventDisableTiming | hipEventDisableSystemFence;
+
 // Make the side stream wait for everything issued so far on `s` (the producer of a dW GEMM's dY).
 int fork_side(ergm_model_plan* P, hipStream_t s) {
     if (P->dry) return ERGM_OK;
@@ -309,8 +313,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->ev_fork = nullptr;
     P->ev_join.assign(d.n_layer + 3, nullptr);
     bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming) == hipSuccess;
-    for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
+    for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
         ergm_model_destroy(P);
         return fail(ERGM_EHIP, "model_create: stream/event creation failed");

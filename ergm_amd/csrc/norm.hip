@@ -79,46 +79,64 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
         gm[i] = c < E ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0, 0, 0, 0);
     }
     const float inv_e = 1.0f / (float)E;
-    const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD;
-    for (int rr = wave; rr < LN_ROWS_PER_BLOCK_BWD; rr += 4) {
-        const int row = r0 + rr;
-        if (row >= rows) break;
-        const float mu = mean_in[row], rs = rstd_in[row];
-        float4 xh[NV], g[NV], d[NV];
-        float s1 = 0.f, s2 = 0.f;
+    // each wave owns RPW = LN_ROWS_PER_BLOCK_BWD/4 rows and issues every load of all of them (x, dy and
+    // the residual gradient it adds into) before the first reduction, so the HBM latency is paid once
+    constexpr int RPW = LN_ROWS_PER_BLOCK_BWD / 4;
+    const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD + wave * RPW;
+    float4 xh[RPW][NV], d[RPW][NV], o[RPW][NV];
+    float mu[RPW], rs[RPW];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const int row = r0 + j;
+        const bool live = row < rows;
+        mu[j] = live ? mean_in[row] : 0.f;
+        rs[j] = live ? rstd_in[row] : 0.f;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             int c = (i * 64 + lane) * 4;
-            if (c < E) {
-                float4 xv = *reinterpret_cast<const float4*>(x + (size_t)row * E + c);
-                d[i] = *reinterpret_cast<const float4*>(dy + (size_t)row * E + c);
-                xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+            if (live && c < E) {
+                xh[j][i] = *reinterpret_cast<const float4*>(x + (size_t)row * E + c);
+                d[j][i] = *reinterpret_cast<const float4*>(dy + (size_t)row * E + c);
+                o[j][i] = *reinterpret_cast<const float4*>(dres + (size_t)row * E + c);
             } else {
-                d[i] = make_float4(0, 0, 0, 0);
-                xh[i] = make_float4(0, 0, 0, 0);
+                xh[j][i] = d[j][i] = o[j][i] = make_float4(0, 0, 0, 0);
             }
-            g[i] = make_float4(d[i].x * gm[i].x, d[i].y * gm[i].y, d[i].z * gm[i].z, d[i].w * gm[i].w);
-            s1 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const int row = r0 + j;
+        float s1 = 0.f, s2 = 0.f;
+        float4 g[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            float4& h = xh[j][i];
+            const float4 dv = d[j][i];
+            h = make_float4((h.x - mu[j]) * rs[j], (h.y - mu[j]) * rs[j], (h.z - mu[j]) * rs[j], (h.w - mu[j]) * rs[j]);
+            g[i] = make_float4(dv.x * gm[i].x, dv.y * gm[i].y, dv.z * gm[i].z, dv.w * gm[i].w);
+            s1 += (g[i].x * h.x + g[i].y * h.y) + (g[i].z * h.z + g[i].w * h.w);
             s2 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
-            pg[i].x += d[i].x * xh[i].x; pg[i].y += d[i].y * xh[i].y;
-            pg[i].z += d[i].z * xh[i].z; pg[i].w += d[i].w * xh[i].w;
-            pb[i].x += d[i].x; pb[i].y += d[i].y; pb[i].z += d[i].z; pb[i].w += d[i].w;
+            pg[i].x += dv.x * h.x; pg[i].y += dv.y * h.y;
+            pg[i].z += dv.z * h.z; pg[i].w += dv.w * h.w;
+            pb[i].x += dv.x; pb[i].y += dv.y; pb[i].z += dv.z; pb[i].w += dv.w;
         }
         const float c1 = wave_sum(s1) * inv_e, c2 = wave_sum(s2) * inv_e;
+        if (row >= rows) continue;
+        const float r = rs[j];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             int c = (i * 64 + lane) * 4;
             if (c < E) {
-                float* dp = dres + (size_t)row * E + c;
-                float4 o = *reinterpret_cast<float4*>(dp);
-                o.x += rs * (g[i].x - c2 - xh[i].x * c1);
-                o.y += rs * (g[i].y - c2 - xh[i].y * c1);
-                o.z += rs * (g[i].z - c2 - xh[i].z * c1);
-                o.w += rs * (g[i].w - c2 - xh[i].w * c1);
-                *reinterpret_cast<float4*>(dp) = o;
+                float4 v = o[j][i];
+                const float4 h = xh[j][i];
+                v.x += r * (g[i].x - c2 - h.x * c1);
+                v.y += r * (g[i].y - c2 - h.y * c1);
+                v.z += r * (g[i].z - c2 - h.z * c1);
+                v.w += r * (g[i].w - c2 - h.w * c1);
+                *reinterpret_cast<float4*>(dres + (size_t)row * E + c) = v;
                 if (dres_b) {
                     bf16x4 ob;
-                    ob[0] = f2bf(o.x); ob[1] = f2bf(o.y); ob[2] = f2bf(o.z); ob[3] = f2bf(o.w);
+                    ob[0] = f2bf(v.x); ob[1] = f2bf(v.y); ob[2] = f2bf(v.z); ob[3] = f2bf(v.w);
                     *reinterpret_cast<bf16x4*>(dres_b + (size_t)row * E + c) = ob;
                 }
             }

@@ -28,6 +28,7 @@ class DPSync:
         self.buckets = buckets or []
         self._works: List = []
         self._stream = None
+        self._events: List = []
 
     @property
     def world(self) -> int:
@@ -67,10 +68,13 @@ class DPSync:
         if grad.is_cuda:
             cur = torch.cuda.current_stream(grad.device)
             side = self._side(grad.device)
-            ev = torch.cuda.Event()
-            ev.record(cur)
+            while len(self._events) <= k:
+                from ._lib import HipEvent
+                self._events.append(HipEvent(sync=True))
+            ev = self._events[k]  # reused every step: the wait below is enqueued right after the record
+            ev.record(cur.cuda_stream)
+            ev.wait(side.cuda_stream)
             with torch.cuda.stream(side):
-                side.wait_event(ev)
                 if self.active:
                     import torch.distributed as dist
                     work = dist.all_reduce(grad[a:b], group=self.pg, async_op=True)

@@ -170,13 +170,14 @@ def emotion_head(h, W, labels, B, S, B_global=None, dh=None, grad_scale=None):
     return logits, loss_sum, dW
 
 
-def adamw_step(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step):
-    """One torch.optim.AdamW step (flat fp32 buffers), bias corrections formed in double like torch."""
+def adamw_step(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, max_blocks=0):
+    """One torch.optim.AdamW step (flat fp32 buffers), bias corrections formed in double like torch.
+    ``max_blocks`` > 0 caps the grid (for updates overlapped with other work)."""
     import math
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step
     L.call("ergm_adamw_step", _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
-           weight_decay, lr / bc1, math.sqrt(bc2), _stream(p.device))
+           weight_decay, lr / bc1, math.sqrt(bc2), int(max_blocks), _stream(p.device))
 
 
 def cast_bf16(src, dst):

@@ -39,6 +39,7 @@ class FusedAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.model = model  # when given, its bf16 shadow is refreshed in the same pass
         self._applied = set()
+        self.overlap_blocks = 0  # grid cap of the overlapped per-bucket update (CUs it may occupy)
         if overlap:
             if model is None:
                 raise ValueError("overlap=True needs model=")
@@ -70,9 +71,10 @@ class FusedAdamW(torch.optim.Optimizer):
         m, v, g, shadow = st["exp_avg"], st["exp_avg_sq"], model.grad_buf, model.flat_b16
         lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
         self._applied.add(id(flat))
+        nb = self.overlap_blocks
 
         def post(a, b):
-            ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t)
+            ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t, nb)
         return post
 
     @torch.no_grad()

@@ -163,10 +163,12 @@ int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
 
 /* torch.optim.AdamW step over flat fp32 arrays; also refreshes the bf16 shadow copy.
  * Arithmetic in torch's order: p*=(1-lr·wd); m=lerp(m,g,1-β1); v=β2·v+(1-β2)g²;
- * p -= step_size · m / (sqrt(v)/bc2_sqrt + eps), step_size = lr/(1-β1^t), bc2_sqrt = sqrt(1-β2^t). */
+ * p -= step_size · m / (sqrt(v)/bc2_sqrt + eps), step_size = lr/(1-β1^t), bc2_sqrt = sqrt(1-β2^t).
+ * max_blocks > 0 caps the grid (grid-stride loop): an update running concurrently with the backward
+ * on another stream then occupies only that many CUs instead of flooding the chip; 0 = full grid. */
 int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
                     float beta1, float beta2, float eps, float weight_decay, float step_size,
-                    float bc2_sqrt, void* stream);
+                    float bc2_sqrt, int max_blocks, void* stream);
 /* bf16 shadow copy of fp32 values: dst[i] = bf16(src[i]). */
 int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream);
 /* y[i] += x[i] (f32), used to accumulate gradients across backward calls. */
