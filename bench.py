@@ -27,6 +27,22 @@ sys.path.insert(0, HERE)
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+
+
+def pmc_traffic(probe: int):
+    """HBM bytes per launch of the probed kernel from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from separate rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes).  None when no summary covers the probe."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "r*_pmc_traffic.json")))
+    if probe != 1 or not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f).get("lm_head_fwd")
+    if not rec:
+        return None, None
+    return round(rec["hbm_bytes"]), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {
     # name: (S, turns, batch per GPU, description)
     "c2": (128, 5, 16, "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
@@ -173,6 +189,7 @@ def main():
     probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
                   2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
     achieved = probe_flops / (probe_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(args.probe)
     step_flops = flops_per_utterance(S) * B
     rec = {
         "metric": "utterances/sec training, MELD-shape synthetic batch, 1/2/4/8 MI355X",
@@ -192,7 +209,8 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": round(achieved, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "traffic": None, "avg_launch_ms": round(probe_ms, 4),
+                     "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                     "avg_launch_ms": round(probe_ms, 4),
                      "flops_per_launch": probe_flops},
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),

@@ -57,6 +57,7 @@ _SIGS = {
     "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
     "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "ergm_attn_tune": (i32, [i32]),
     "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),
     "ergm_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, f32, vp]),
     "ergm_layernorm_bwd_workspace_size": (sz, [i32, i32]),

@@ -13,6 +13,9 @@
 // permuted identically on both operands) and Vᵀ comes from the LDS V tile by ds_read_b64_tr_b16.
 // Backward: dK/dV kernel (workgroup = 64 keys, loops over query tiles, P recomputed from the
 // forward LSE) + dQ kernel (workgroup = 64 queries, loops over key tiles); no atomics, deterministic.
+// Sequences of at most 128 (the training path: S = 128 tokens, 128 caption rows) take the
+// *_short kernels instead: one 8-wave workgroup per (b, h) holding every operand in LDS, the whole
+// backward in one launch.  Both paths evaluate every product in the same order (bit-identical).
 #include "common.h"
 
 namespace ergm {
@@ -90,6 +93,78 @@ struct AttnArgs {
     float scale;
 };
 
+// One 64-key tile of the online-softmax forward for this lane's query q (keys key0..key0+63 of the
+// staged sK / sV tiles): scores, running max / sum update, Oᵀ += Vᵀ·Pᵀ.
+template <bool CAUSAL>
+__device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int key0, int q, int Sk, float scale,
+                                            const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l) {
+    const int g = (threadIdx.x & 63) >> 4;
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        s[kb] = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s[kb]);
+        s[kb] = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s[kb]);
+    }
+    // s[kb][r] = score(key = key0 + kb*16 + 4g + r, query q)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int key = key0 + kb * 16 + 4 * g + r;
+            float x = s[kb][r] * scale;
+            bool masked = key >= Sk || (CAUSAL && key > q);
+            x = masked ? -INFINITY : x;
+            s[kb][r] = x;
+            mx = fmaxf(mx, x);
+        }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float muse = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = __expf(m - muse);
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float p = __expf(s[kb][r] - muse);
+            s[kb][r] = p;
+            rs += p;
+        }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    // Oᵀ[d][q] += Σ_key V[key][d] P[q][key]
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        bf16x8 pb = pack_p(s[2 * half], s[2 * half + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = MFMA16(tr_frag(sV, 32 * half, d * 16), pb, o[d]);
+    }
+}
+
+// Normalised output row (bf16) and the log-sum-exp of this lane's query.
+__device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q, const f32x4 (&o)[4], float m,
+                                          float l) {
+    const int g = (threadIdx.x & 63) >> 4;
+    if (q >= a.Sq) return;
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    __bf16* Ob = a.out + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        bf16x4 w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = f2bf(o[d][r] * inv);
+        *reinterpret_cast<bf16x4*>(Ob + d * 16 + 4 * g) = w;
+    }
+    if (g == 0) a.lse[((size_t)b * a.H + h) * a.Sq + q] = m + logf(l);
+}
+
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) char sK[AT_TILE_BYTES];
@@ -124,66 +199,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         stage_tile(sK, Kb, a.ldk, key0, a.Sk, 0);
         stage_tile(sV, Vb, a.ldv, key0, a.Sk, 0);
         __syncthreads();
-        f32x4 s[4];
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            s[kb] = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s[kb]);
-            s[kb] = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s[kb]);
-        }
-        // s[kb][r] = score(key = key0 + kb*16 + 4g + r, query q)
-        float mx = -INFINITY;
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int key = key0 + kb * 16 + 4 * g + r;
-                float x = s[kb][r] * a.scale;
-                bool masked = key >= a.Sk || (CAUSAL && key > q);
-                x = masked ? -INFINITY : x;
-                s[kb][r] = x;
-                mx = fmaxf(mx, x);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m, mx);
-        const float muse = mnew == -INFINITY ? 0.f : mnew;
-        const float alpha = __expf(m - muse);
-        float rs = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float p = __expf(s[kb][r] - muse);
-                s[kb][r] = p;
-                rs += p;
-            }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-        l = l * alpha + rs;
-        m = mnew;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) o[d] *= alpha;
-        // Oᵀ[d][q] += Σ_key V[key][d] P[q][key]
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            bf16x8 pb = pack_p(s[2 * half], s[2 * half + 1]);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) o[d] = MFMA16(tr_frag(sV, 32 * half, d * 16), pb, o[d]);
-        }
+        fwd_kv_tile<CAUSAL>(sK, sV, key0, q, a.Sk, a.scale, qf, o, m, l);
     }
-    if (q < a.Sq) {
-        const float inv = l > 0.f ? 1.0f / l : 0.f;
-        __bf16* Ob = a.out + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            bf16x4 w;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = f2bf(o[d][r] * inv);
-            *reinterpret_cast<bf16x4*>(Ob + d * 16 + 4 * g) = w;
-        }
-        if (g == 0) a.lse[((size_t)b * a.H + h) * a.Sq + q] = m + logf(l);
-    }
+    fwd_store(a, b, h, q, o, m, l);
 }
 
 // delta[b,h,q] = Σ_d dO·O
@@ -401,6 +419,233 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     }
 }
 
+// ---- short sequences (Sq, Sk <= 128): the whole backward of one (b, h) in one workgroup ----------
+// 8 waves.  Q, dO, K, V (up to 128 rows each) are staged in LDS once; δ and the LSE per query too.
+// Phase 1 (keys-major): wave w owns keys 16w..16w+15 and accumulates dK, dV over every query, as
+// attn_bwd_dkv_kernel does, and also stores its dS (bf16) key-major into LDS.  Phase 2 (queries-
+// major): wave w owns queries 16w..16w+15: dQᵀ = Kᵀ·dSᵀ, both operands read transposed from LDS.
+// One launch instead of two, no re-staging of Q/dO per key tile, no recomputation of P for dQ.
+constexpr int AS_MAX = 128;                          // max Sq / Sk of the fused path
+constexpr int AS_TILES = AS_MAX / AT_T;              // 64-row tiles per operand
+constexpr int AS_OPER = AS_TILES * AT_TILE_BYTES;    // 16 KiB per staged operand
+constexpr int AS_LDS = 4 * AS_OPER + AS_TILES * AS_TILES * AT_TILE_BYTES + 2 * AS_MAX * 4;  // 96 KiB + 1 KiB
+
+// 128 rows x 64 dims of a token-major operand as two swizzled 64-row tiles (rows >= nrows are zero):
+// the loads are issued first (2 x 16 B per thread), then written to LDS, so several staged operands
+// can have all their loads in flight together (load_rows ... load_rows, then put_rows ...).
+struct Rows128 {
+    uint4 v[2];
+};
+__device__ __forceinline__ Rows128 load_rows(const __bf16* base, int ld, int nrows) {
+    Rows128 r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int c = threadIdx.x + i * 512, row = c >> 3, ch = c & 7;
+        r.v[i] = row < nrows ? *reinterpret_cast<const uint4*>(base + (size_t)row * ld + ch * 8) : make_uint4(0, 0, 0, 0);
+    }
+    return r;
+}
+__device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int c = threadIdx.x + i * 512, row = c >> 3, ch = c & 7;
+        *reinterpret_cast<uint4*>(lds + (row >> 6) * AT_TILE_BYTES + tile_off(row & 63, ch)) = r.v[i];
+    }
+}
+
+// Forward for Sq, Sk <= 128: one workgroup (8 waves, 16 queries each) per (b, h); K and V staged once.
+template <bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_fwd_short_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) char sK[AS_OPER];
+    __shared__ __attribute__((aligned(16))) char sV[AS_OPER];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int q = wave * 16 + i16;
+    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
+    bf16x8 qf[2];
+    qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
+    qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
+    {
+        const Rows128 rk = load_rows(a.k + (size_t)b * a.Sk * a.ldk + h * AT_D, a.ldk, a.Sk);
+        const Rows128 rv = load_rows(a.v + (size_t)b * a.Sk * a.ldv + h * AT_D, a.ldv, a.Sk);
+        put_rows(sK, rk);
+        put_rows(sV, rv);
+    }
+    __syncthreads();
+    f32x4 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    int nkt = (a.Sk + AT_T - 1) / AT_T;
+    if (CAUSAL) nkt = min(nkt, (wave * 16 + 15) / AT_T + 1);
+    for (int kt = 0; kt < nkt; ++kt)
+        fwd_kv_tile<CAUSAL>(sK + kt * AT_TILE_BYTES, sV + kt * AT_TILE_BYTES, kt * AT_T, q, a.Sk, a.scale, qf, o, m,
+                            l);
+    fwd_store(a, b, h, q, o, m, l);
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sQ = smem;
+    char* sdO = sQ + AS_OPER;
+    char* sK = sdO + AS_OPER;
+    char* sV = sK + AS_OPER;
+    char* sdS = sV + AS_OPER;                          // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
+    float* sL = reinterpret_cast<float*>(sdS + AS_TILES * AS_TILES * AT_TILE_BYTES);
+    float* sD = sL + AS_MAX;
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
+    const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
+    const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
+    const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
+    {
+        const Rows128 rq = load_rows(Qb, a.ldq, a.Sq);
+        const Rows128 rdo = load_rows(dOb, a.lddo, a.Sq);
+        const Rows128 rk = load_rows(Kb, a.ldk, a.Sk);
+        const Rows128 rv = load_rows(Vb, a.ldv, a.Sk);
+        // δ[q] = Σ_d dO·O (4 threads per query, 16 dims each) and the forward LSE
+        const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
+        bf16x8 x0, x1, y0, y1;
+        float lse = 0.f;
+        if (ql < a.Sq) {
+            const __bf16* od = a.o + ((size_t)b * a.Sq + ql) * a.ldo + h * AT_D + part * 16;
+            const __bf16* dd = dOb + (size_t)ql * a.lddo + part * 16;
+            x0 = *reinterpret_cast<const bf16x8*>(dd);
+            x1 = *reinterpret_cast<const bf16x8*>(dd + 8);
+            y0 = *reinterpret_cast<const bf16x8*>(od);
+            y1 = *reinterpret_cast<const bf16x8*>(od + 8);
+            lse = a.lse[((size_t)b * a.H + h) * a.Sq + ql];
+        }
+        put_rows(sQ, rq);
+        put_rows(sdO, rdo);
+        put_rows(sK, rk);
+        put_rows(sV, rv);
+        float dsum = 0.f;
+        if (ql < a.Sq) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f(x0[j]) * bf2f(y0[j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f(x1[j]) * bf2f(y1[j]);
+        }
+        dsum += __shfl_xor(dsum, 1, 64);
+        dsum += __shfl_xor(dsum, 2, 64);
+        if (part == 0) {
+            sL[ql] = lse;
+            sD[ql] = dsum;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 1: this wave's 16 keys
+    {
+        const int key = wave * 16 + i16;
+        const int kt = wave >> 2;                      // key tile of this wave
+        const int krow = (wave & 3) * 16 + i16;        // row inside that tile
+        bf16x8 kf[2], vf[2];
+        kf[0] = row_frag(sK + kt * AT_TILE_BYTES, (wave & 3) * 16, 0);
+        kf[1] = row_frag(sK + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
+        vf[0] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 0);
+        vf[1] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
+        f32x4 dk[4], dv[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+            dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        const int nqt = (a.Sq + AT_T - 1) / AT_T;
+        for (int qt = CAUSAL ? kt : 0; qt < nqt; ++qt) {
+            const char* tQ = sQ + qt * AT_TILE_BYTES;
+            const char* tdO = sdO + qt * AT_TILE_BYTES;
+            char* tS = sdS + (kt * AS_TILES + qt) * AT_TILE_BYTES;
+            f32x4 p[4], ds[4];
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb) {
+                f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+                s = MFMA16(row_frag(tQ, qb * 16, 0), kf[0], s);
+                s = MFMA16(row_frag(tQ, qb * 16, 1), kf[1], s);
+                f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
+                dp = MFMA16(row_frag(tdO, qb * 16, 0), vf[0], dp);
+                dp = MFMA16(row_frag(tdO, qb * 16, 1), vf[1], dp);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ql = qt * AT_T + qb * 16 + 4 * g + r;
+                    const bool masked = ql >= a.Sq || key >= a.Sk || (CAUSAL && key > ql);
+                    const float pv = masked ? 0.f : __expf(s[r] * a.scale - sL[ql]);
+                    p[qb][r] = pv;
+                    ds[qb][r] = pv * (dp[r] - sD[ql]);
+                }
+                // dS[key][q..q+3] -> key-major LDS tile (one 8-byte store per lane)
+                bf16x4 w;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) w[r] = f2bf(ds[qb][r]);
+                const int qc = qb * 16 + 4 * g;      // query column inside the tile
+                *reinterpret_cast<bf16x4*>(tS + tile_off(krow, qc >> 3) + (qc & 7) * 2) = w;
+            }
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                bf16x8 pb = pack_p(p[2 * half], p[2 * half + 1]);
+                bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    dv[d] = MFMA16(tr_frag(tdO, 32 * half, d * 16), pb, dv[d]);
+                    dk[d] = MFMA16(tr_frag(tQ, 32 * half, d * 16), sb, dk[d]);
+                }
+            }
+        }
+        if (key < a.Sk) {
+            size_t tok = (size_t)b * a.Sk + key;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                bf16x4 wk, wv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    wk[r] = f2bf(dk[d][r] * a.scale);
+                    wv[r] = f2bf(dv[d][r]);
+                }
+                *reinterpret_cast<bf16x4*>(a.dk + tok * a.lddk + h * AT_D + d * 16 + 4 * g) = wk;
+                *reinterpret_cast<bf16x4*>(a.dv + tok * a.lddv + h * AT_D + d * 16 + 4 * g) = wv;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: this wave's 16 queries, dQᵀ[d][q] = Σ_key K[key][d] dS[key][q]
+    {
+        const int q = wave * 16 + i16;
+        const int qt = wave >> 2, qc0 = (wave & 3) * 16;
+        f32x4 dq[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int nkt = CAUSAL ? qt + 1 : (a.Sk + AT_T - 1) / AT_T;
+        for (int kt = 0; kt < nkt; ++kt) {
+            const char* tK = sK + kt * AT_TILE_BYTES;
+            const char* tS = sdS + (kt * AS_TILES + qt) * AT_TILE_BYTES;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                // rows (keys) of a tile the causal phase 1 never wrote are skipped whole (kt > qt);
+                // inside a diagonal tile masked entries were stored as 0
+                bf16x8 sb = tr_frag(tS, 32 * half, qc0);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) dq[d] = MFMA16(tr_frag(tK, 32 * half, d * 16), sb, dq[d]);
+            }
+        }
+        if (q < a.Sq) {
+            __bf16* out = a.dq + ((size_t)b * a.Sq + q) * a.lddq + h * AT_D;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                bf16x4 w;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) w[r] = f2bf(dq[d][r] * a.scale);
+                *reinterpret_cast<bf16x4*>(out + d * 16 + 4 * g) = w;
+            }
+        }
+    }
+}
+
 static int check_common(const void* q, const void* k, const void* v, int B, int H, int Sq, int Sk, int ldq, int ldk,
                         int ldv, int causal) {
     ERGM_CHECK_ARG(q && k && v, "attn: null argument");
@@ -416,6 +661,15 @@ static int check_common(const void* q, const void* k, const void* v, int B, int 
 
 using namespace ergm;
 
+namespace {
+bool g_attn_generic = false;  // ergm_attn_tune: force the tiled kernels even for short sequences
+}
+
+extern "C" int ergm_attn_tune(int force_generic) {
+    g_attn_generic = force_generic != 0;
+    return ERGM_OK;
+}
+
 extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int causal, void* stream) {
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
@@ -426,8 +680,14 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
     a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
     a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
     a.scale = 0.125f;  // 1/sqrt(64): exact, so x*scale == x / 8.0 (src/model.py:122-125)
-    dim3 grid(cdiv(Sq, AT_T), H, B);
     hipStream_t s = as_stream(stream);
+    if (Sq <= AS_MAX && Sk <= AS_MAX && !g_attn_generic) {
+        dim3 grid(1, H, B);
+        if (causal) hipLaunchKernelGGL(attn_fwd_short_kernel<true>, grid, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(attn_fwd_short_kernel<false>, grid, dim3(512), 0, s, a);
+        return check_launch("attn_fwd");
+    }
+    dim3 grid(cdiv(Sq, AT_T), H, B);
     if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, a);
     return check_launch("attn_fwd");
@@ -452,6 +712,21 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
     a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
     a.scale = 0.125f;
     hipStream_t s = as_stream(stream);
+    if (Sq <= AS_MAX && Sk <= AS_MAX && !g_attn_generic) {
+        static bool attr_set = false;  // benign race: idempotent attribute writes
+        if (!attr_set) {
+            if (hipFuncSetAttribute((const void*)attn_bwd_short_kernel<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess ||
+                hipFuncSetAttribute((const void*)attn_bwd_short_kernel<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess)
+                return fail(ERGM_EHIP, "attn_bwd: cannot raise dynamic LDS limit");
+            attr_set = true;
+        }
+        dim3 grid(1, H, B);
+        if (causal) hipLaunchKernelGGL(attn_bwd_short_kernel<true>, grid, dim3(512), AS_LDS, s, a);
+        else hipLaunchKernelGGL(attn_bwd_short_kernel<false>, grid, dim3(512), AS_LDS, s, a);
+        return check_launch("attn_bwd");
+    }
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
     if (causal) {
         hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, gk, dim3(256), 0, s, a);

@@ -344,6 +344,20 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Wait until at most `after` stages (LPS DMA instructions each) of this wave are still in flight.
+template <int LPS, int MAXA>
+__device__ __forceinline__ void wait_stages(int after) {
+    if constexpr (MAXA > 0) {
+        if (after >= MAXA) {
+            wait_vm<MAXA * LPS>();
+            return;
+        }
+        wait_stages<LPS, MAXA - 1>(after);
+    } else {
+        wait_vm<0>();
+    }
+}
+
 // One 16-B-per-lane LDS-DMA: LDS[lds_addr + 16*lane] = *gsrc.  Issued from inline asm so hipcc does
 // not track it (it would otherwise drain vmcnt before every later ds_read); completion is covered by
 // the explicit counted waits.  M0 is saved/set/restored inside the one statement (guide §5.7).
@@ -403,7 +417,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
     constexpr int STAGE = A_BYTES + B_BYTES;
     constexpr int LPS = GldsTile<BM, A_KM, NW>::PER_WAVE + GldsTile<BN, B_KN, NW>::PER_WAVE;  // vmcnt per stage
-    static_assert(NS >= 2 && NS <= 4, "2..4 stages");
+    static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int nwg = a.tiles_m * a.tiles_n;
@@ -439,9 +453,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     for (int kt = 0; kt < nk; ++kt) {
         // stages this wave issued after kt: min(NS-2, nk-1-kt); wait until stage kt has landed
         const int after = min(NS - 2, nk - 1 - kt);
-        if (after >= 2) wait_vm<2 * LPS>();
-        else if (after == 1) wait_vm<LPS>();
-        else wait_vm<0>();
+        wait_stages<LPS, NS - 2>(after);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot to refill are done
         __builtin_amdgcn_s_barrier();
         if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
@@ -499,6 +511,12 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 4},    // 8
     {256, 128, 4, 2, 2},   // 9
     {128, 128, 4, 2, 2},   // 10 8 waves (32x64 each)
+    {64, 64, 2, 2, 8},     // 11 deep: 7 stages (112 KiB) in flight
+    {128, 64, 2, 2, 6},    // 12
+    {64, 128, 2, 2, 6},    // 13
+    {128, 128, 2, 2, 4},   // 14
+    {128, 128, 4, 2, 4},   // 15 8 waves
+    {256, 128, 4, 2, 4},   // 16 8 waves, 144 KiB
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -593,7 +611,13 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 7: launch_pipe_cfg<7, AKM, BKN, EPI, OB>(a, split, s); break;
         case 8: launch_pipe_cfg<8, AKM, BKN, EPI, OB>(a, split, s); break;
         case 9: launch_pipe_cfg<9, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<10, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 10: launch_pipe_cfg<10, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 11: launch_pipe_cfg<11, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 12: launch_pipe_cfg<12, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 13: launch_pipe_cfg<13, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 14: launch_pipe_cfg<14, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 15: launch_pipe_cfg<15, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<16, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 

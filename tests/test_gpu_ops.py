@@ -146,6 +146,32 @@ def test_attention_fwd_bwd(gpu, B, H, S, causal):
         assert _rel(heads(got), want) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,Sq,Sk,causal", [(2, 12, 128, 128, True), (2, 12, 128, 128, False), (3, 2, 100, 40, False),
+                                              (2, 3, 64, 128, False), (2, 2, 72, 72, True), (1, 1, 17, 17, True)])
+def test_attention_bwd_short_matches_tiled(gpu, B, H, Sq, Sk, causal):
+    """The one-workgroup-per-(b,h) backward (Sq, Sk <= 128) computes every product in the same order
+    as the tiled dK/dV + dQ kernels: the two paths agree bit for bit."""
+    E = 64 * H
+    torch.manual_seed(Sq * 7 + Sk + H)
+    q = torch.randn(B * Sq, E, device=gpu).bfloat16()
+    kv = torch.randn(B * Sk, 2 * E, device=gpu).bfloat16()
+    k, v = kv[:, :E], kv[:, E:]
+    o, lse = ops.attn_fwd(q, k, v, B, H, Sq, Sk, causal)
+    dout = torch.randn(B * Sq, E, device=gpu).bfloat16()
+    lib = L.load()
+    short = ops.attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal)
+    L.check(lib.ergm_attn_tune(1), "attn_tune")
+    try:
+        o2, lse2 = ops.attn_fwd(q, k, v, B, H, Sq, Sk, causal)
+        tiled = ops.attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal)
+    finally:
+        L.check(lib.ergm_attn_tune(0), "attn_tune")
+    torch.cuda.synchronize()
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    for a, b in zip(short, tiled):
+        assert torch.equal(a, b)
+
+
 def test_attention_cross_strided(gpu):
     """Cross-attention reading K/V straight out of a stacked [T, L*2E] projection buffer."""
     B, H, S, Lyr = 2, 4, 128, 3

@@ -42,11 +42,43 @@ SHAPES = [
     ("bwd dcap", 1, T, E, L2E, MK, L2E, NK, L2E, L.EPI_NONE, FP),
 ]
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
-        (256, 128), (128, 128)]
+        (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128), (256, 128)]
 REPS = 20
 
 
+def blas_compare():
+    """torch.matmul (hipBLASLt) on the same shapes/transposes, bf16 in and out, vs ergm_gemm auto."""
+    dev = torch.device("cuda:0")
+    tot_b = tot_e = 0.0
+    for (name, cnt, M, N, K, al, lda, bl, ldb, epi, cdt) in SHAPES:
+        a = torch.randn(M, K, device=dev).bfloat16() if al == MK else torch.randn(K, M, device=dev).bfloat16().t()
+        b = torch.randn(K, N, device=dev).bfloat16() if bl == KN else torch.randn(N, K, device=dev).bfloat16().t()
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            c = a @ b
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(REPS):
+                torch.matmul(a, b, out=c)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        tb = e0.elapsed_time(e1) / (3 * REPS) * 1e3
+        tot_b += tb * cnt
+        print(f"{name:22s} x{cnt:2d} M={M:5d} N={N:5d} K={K:5d}  hipBLASLt {tb:8.1f}us "
+              f"({2.0 * M * N * K / tb / 1e6:6.0f} TF)", flush=True)
+    print(f"per-step GEMM time hipBLASLt (bf16 out, no epilogue): {tot_b / 1e3:.3f} ms")
+
+
 def main():
+    if "--blas" in sys.argv:
+        return blas_compare()
     quick = "--quick" in sys.argv
     dev = torch.device("cuda:0")
     lib = L.load()

@@ -1,0 +1,88 @@
+"""HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of bench.py.
+
+Run on the GPU box (each counter in its own pass, kernel-trace only, no other tracing):
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py ...
+then:  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r01_pmc_traffic.json
+
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md, "HBM"): rocprofv3 reports FETCH_SIZE / WRITE_SIZE in
+KiB; on gfx950 FETCH_SIZE counts exactly half the bytes of wide coalesced streaming reads, so it is
+doubled.  The AdamW kernel (30 B/param of pure streaming: 16 B read + 14 B written) is reported beside
+the GEMM as the calibration of both corrections.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    per = defaultdict(list)  # kernel name -> [value per dispatch]
+    for f in files:
+        acc = defaultdict(float)
+        names = {}
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            key = (f, r["Dispatch_Id"])
+            acc[key] += float(r["Counter_Value"])   # summed over dimensions (XCD/channel) if split
+            names[key] = r["Kernel_Name"]
+        for key, v in acc.items():
+            per[names[key]].append(v * 1024.0)      # KiB -> bytes
+    return per
+
+
+def main():
+    fdir, wdir, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    fetch = _load(fdir, "FETCH_SIZE")
+    write = _load(wdir, "WRITE_SIZE")
+    from ergm_amd.config import gpt2_small
+    from ergm_amd.params import build_layout
+    cfg = gpt2_small()
+    T, E, Vp = 16 * 128, cfg.n_embd, 50304
+    n_flat = build_layout(cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.inner, cfg.n_positions).total
+
+    def pick(pred):
+        ks = [k for k in fetch if pred(k)]
+        if not ks:
+            return None
+        k = ks[0]
+        fb = 2.0 * statistics.median(fetch[k])
+        wb = statistics.median(write.get(k, [0.0]))
+        return k, fb, wb
+
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of bench.py; "
+                     "FETCH_SIZE doubled (gfx950 streaming-read correction), KiB -> bytes; median over dispatches"}
+    lm = pick(lambda k: "gemm_pipe_kernel<256, 256" in k)
+    if lm:
+        k, fb, wb = lm
+        alg = 2 * T * E + 2 * Vp * E + 2 * T * Vp   # A [T,E] + wte [Vp,E] bf16 read, logits [T,Vp] bf16 written
+        res["lm_head_fwd"] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+                              "algorithmic_bytes": alg, "ratio": (fb + wb) / alg}
+    ad = pick(lambda k: "adamw_kernel" in k)
+    if ad:
+        k, fb, wb = ad
+        res["adamw_calibration"] = {"kernel": k, "n_params": n_flat, "fetch_bytes": fb, "write_bytes": wb,
+                                    "expected_read": 16 * n_flat, "expected_write": 14 * n_flat,
+                                    "read_ratio": fb / (16 * n_flat), "write_ratio": wb / (14 * n_flat)}
+    allk = {}
+    for k in fetch:
+        allk[k.split("(")[0][:90]] = {"fetch_bytes": 2.0 * statistics.median(fetch[k]),
+                                      "write_bytes": statistics.median(write.get(k, [0.0])),
+                                      "dispatches": len(fetch[k])}
+    res["per_kernel_median"] = allk
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_kernel_median"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

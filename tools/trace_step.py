@@ -45,3 +45,29 @@ if "--gaps" in sys.argv:
         g = (int(q['Start_Timestamp']) - int(p['End_Timestamp'])) / 1e3
         if g > 8:
             print(f"gap {g:7.1f} us at t={(int(p['End_Timestamp']) - t0) / 1e3:8.1f}: {short(p)} -> {short(q)}")
+# main-stream time by phase and kernel class
+if "--phases" in sys.argv:
+    main_q = max(by_q, key=by_q.get)
+    ph, cur = defaultdict(lambda: defaultdict(float)), "forward"
+    for r in step:
+        n = r['Kernel_Name']
+        if 'xent_kernel' in n:
+            cur = "loss+head bwd"
+        elif 'attn_bwd' in n and cur == "loss+head bwd":
+            cur = "layers bwd"
+        elif 'embed_sort' in n:
+            cur = "embed bwd"
+        q = r['Queue_Id'] + '/' + r['Stream_Id']
+        cls = ('gemm' if 'gemm' in n or 'splitk' in n else 'attn' if 'attn' in n else
+               'ln' if 'ln_' in n else 'adamw' if 'adamw' in n else 'other')
+        ph[(cur, 'main' if q == main_q else 'side')][cls] += (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+    for k, v in ph.items():
+        print(f"{k[0]:14s} {k[1]:5s} total {sum(v.values()):8.1f} us  " +
+              "  ".join(f"{c}={t:.0f}" for c, t in sorted(v.items(), key=lambda kv: -kv[1])))
+if "--gapstats" in sys.argv:
+    main_q = max(by_q, key=by_q.get)
+    ms = [r for r in step if r['Queue_Id'] + '/' + r['Stream_Id'] == main_q]
+    gs = [(int(q['Start_Timestamp']) - int(p['End_Timestamp'])) / 1e3 for p, q in zip(ms, ms[1:])]
+    import statistics as _st
+    print(f"main-stream gaps: n={len(gs)} sum={sum(gs):.1f} us median={_st.median(gs):.2f} us "
+          f"sum(<8us)={sum(g for g in gs if g < 8):.1f} us sum(>=8us)={sum(g for g in gs if g >= 8):.1f} us")
