@@ -72,12 +72,14 @@ _SIGS = {
     "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ergm_loss_finalize": (i32, [vp, i32, vp, vp, i32, vp, vp]),
     "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
+    "ergm_adamw_rows": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, i32, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
     "ergm_axpy": (i32, [vp, vp, sz, f32, vp]),
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),
     "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
+    "ergm_model_set_row_flags": (i32, [vp, vp, i32]),
     "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
     "ergm_model_forward": (i32, [vp, vp, vp, vp, i32, vp]),
     "ergm_model_backward_head": (i32, [vp, vp, vp]),

@@ -7,6 +7,8 @@
 // and refreshes the bf16 shadow copy the GEMMs read, in the same pass (HBM-bound: 30 B/param).
 #include "common.h"
 
+#include <algorithm>
+
 namespace ergm {
 
 __device__ __forceinline__ void adamw_one(float4& pp, const float4& gg, float4& mm, float4& vv, bf16x4& ob, float decay,
@@ -88,6 +90,29 @@ __global__ __launch_bounds__(256) void axpy_kernel(const float4* __restrict__ x,
     }
 }
 
+// Row-selective AdamW over a [rows][row_len] block: row r is updated iff (flag[r] != 0) == select.
+// One workgroup per row (grid-stride): a skipped row costs one flag byte.
+__global__ __launch_bounds__(256) void adamw_rows_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                                                         float4* __restrict__ m, float4* __restrict__ v,
+                                                         bf16x4* __restrict__ pb, int rows, int row4,
+                                                         const uint8_t* __restrict__ flag, int select, float decay,
+                                                         float one_m_b1, float b2, float one_m_b2, float eps,
+                                                         float step_size, float bc2_sqrt) {
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+        if ((flag[r] != 0) != (select != 0)) continue;
+        for (int c = threadIdx.x; c < row4; c += 256) {
+            const size_t i = (size_t)r * row4 + c;
+            float4 pp = p[i], gg = nt_load4(g + i), mm = m[i], vv = v[i];
+            bf16x4 o;
+            adamw_one(pp, gg, mm, vv, o, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+            p[i] = pp;
+            m[i] = mm;
+            v[i] = vv;
+            if (pb) pb[i] = o;
+        }
+    }
+}
+
 static unsigned grid_for(size_t n4) {
     size_t blocks = (n4 + 255) / 256;
     return (unsigned)(blocks < 8192 ? (blocks ? blocks : 1) : 8192);
@@ -122,6 +147,26 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2, one_m_b2, eps, step_size,
                        bc2_sqrt);
     return check_launch("adamw");
+}
+
+extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
+                               const void* row_flag, int select, float lr, float beta1, float beta2, float eps,
+                               float weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
+    ERGM_CHECK_ARG(p && g && m && v && row_flag, "adamw_rows: null argument");
+    ERGM_CHECK_ARG(rows >= 0 && row_len > 0 && row_len % 4 == 0, "adamw_rows: row_len must be a positive multiple of 4");
+    ERGM_CHECK_ARG(max_blocks >= 0, "adamw_rows: max_blocks must be >= 0");
+    ERGM_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), "adamw_rows: 16-byte alignment");
+    ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw_rows: bf16 copy alignment");
+    if (rows == 0) return ERGM_OK;
+    float decay = (float)(1.0 - (double)lr * (double)weight_decay);
+    float one_m_b1 = (float)(1.0 - (double)beta1);
+    float one_m_b2 = (float)(1.0 - (double)beta2);
+    unsigned grid = (unsigned)std::min(rows, 8192);
+    if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
+    hipLaunchKernelGGL(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, rows, row_len / 4, (const uint8_t*)row_flag, select,
+                       decay, one_m_b1, beta2, one_m_b2, eps, step_size, bc2_sqrt);
+    return check_launch("adamw_rows");
 }
 
 extern "C" int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream) {

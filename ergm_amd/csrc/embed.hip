@@ -55,9 +55,10 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 constexpr int SORT_MAX = 16384;  // entries handled by the single-workgroup LDS sort (128 KiB of u64)
 
 // keys = (vocab id << 32) | entry, entry in [0, 3T): [0,T) input ids, [T,2T) token types, [2T,3T) captions
+// row_flag (optional, pre-zeroed, one byte per vocab row): set to 1 for every row the lookups touch.
 __global__ __launch_bounds__(1024) void embed_sort_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
                                                           const int64_t* __restrict__ cap_ids, int T, int V, int npad,
-                                                          uint64_t* __restrict__ out) {
+                                                          uint64_t* __restrict__ out, uint8_t* __restrict__ row_flag) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint64_t* key = reinterpret_cast<uint64_t*>(smem);
     const int n = 3 * T;
@@ -86,12 +87,17 @@ __global__ __launch_bounds__(1024) void embed_sort_kernel(const int64_t* __restr
             __syncthreads();
         }
     }
-    for (int i = threadIdx.x; i < n; i += 1024) out[i] = key[i];
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const uint64_t k = key[i];
+        out[i] = k;
+        if (row_flag && k != ~0ull) row_flag[k >> 32] = 1;
+    }
 }
 
 // Pass 1: one workgroup per chunk of SEG_CH sorted positions.  Every maximal run of equal ids inside
-// the chunk is summed in position order and written to part[run start].
-constexpr int SEG_CH = 64;
+// the chunk is summed in position order and written to part[run start].  The chunk's rows are all
+// loaded before the (ordered) sum, so the SEG_CH row reads are in flight together.
+constexpr int SEG_CH = 16;
 
 __device__ __forceinline__ const float* seg_row(uint64_t key, int T, const float* dh0, const float* dcap, int E) {
     int e = (int)(uint32_t)key;
@@ -102,37 +108,45 @@ template <int NC>
 __global__ __launch_bounds__(256) void embed_runsum_kernel(const uint64_t* __restrict__ keys, int n, int T,
                                                            const float* __restrict__ dh0, const float* __restrict__ dcap,
                                                            float* __restrict__ part, int E) {
-    const int p0 = blockIdx.x * SEG_CH, p1 = min(n, p0 + SEG_CH);
+    const int p0 = blockIdx.x * SEG_CH;
+    if (keys[p0] == ~0ull) return;
+    uint64_t kq[SEG_CH];
+    float v[SEG_CH][NC];
+#pragma unroll
+    for (int q = 0; q < SEG_CH; ++q) {
+        kq[q] = p0 + q < n ? keys[p0 + q] : ~0ull;
+        const float* row = kq[q] != ~0ull ? seg_row(kq[q], T, dh0, dcap, E) : nullptr;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const int c = threadIdx.x + j * 256;
+            v[q][j] = row && c < E ? row[c] : 0.f;
+        }
+    }
     float acc[NC];
-    int start = p0;
-    uint32_t id = (uint32_t)(keys[p0] >> 32);
 #pragma unroll
     for (int j = 0; j < NC; ++j) acc[j] = 0.f;
-    for (int q = p0; q < p1; ++q) {
-        const uint64_t kq = keys[q];
-        if (kq == ~0ull) break;
-        const uint32_t iq = (uint32_t)(kq >> 32);
+    int start = p0;
+    uint32_t id = (uint32_t)(kq[0] >> 32);
+#pragma unroll
+    for (int q = 0; q < SEG_CH; ++q) {
+        if (kq[q] == ~0ull) break;
+        const uint32_t iq = (uint32_t)(kq[q] >> 32);
         if (iq != id) {
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
-                int c = threadIdx.x + j * 256;
+                const int c = threadIdx.x + j * 256;
                 if (c < E) part[(size_t)start * E + c] = acc[j];
                 acc[j] = 0.f;
             }
-            start = q;
+            start = p0 + q;
             id = iq;
         }
-        const float* row = seg_row(kq, T, dh0, dcap, E);
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            int c = threadIdx.x + j * 256;
-            if (c < E) acc[j] += row[c];
-        }
+        for (int j = 0; j < NC; ++j) acc[j] += v[q][j];
     }
-    if (keys[p0] == ~0ull) return;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-        int c = threadIdx.x + j * 256;
+        const int c = threadIdx.x + j * 256;
         if (c < E) part[(size_t)start * E + c] = acc[j];
     }
 }
@@ -154,14 +168,28 @@ __global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __res
         int c = threadIdx.x + j * 256;
         acc[j] = c < E ? part[(size_t)p * E + c] : 0.f;
     }
-    for (int q = (p / SEG_CH + 1) * SEG_CH; q < n; q += SEG_CH) {
-        uint64_t kq = keys[q];
-        if (kq == ~0ull || (uint32_t)(kq >> 32) != id) break;
+    // the run continues into chunk q while keys[q] (the chunk's first key) still has this id; keys are
+    // sorted, so that holds for a prefix of the following chunks: fetch 8 chunk partials at a time
+    constexpr int G = 8;
+    for (int q0 = (p / SEG_CH + 1) * SEG_CH; q0 < n; q0 += G * SEG_CH) {
+        bool more[G];
+        float v[G][NC];
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            int c = threadIdx.x + j * 256;
-            if (c < E) acc[j] += part[(size_t)q * E + c];
+        for (int i = 0; i < G; ++i) {
+            const int q = q0 + i * SEG_CH;
+            const uint64_t kq = q < n ? keys[q] : ~0ull;
+            more[i] = kq != ~0ull && (uint32_t)(kq >> 32) == id;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const int c = threadIdx.x + j * 256;
+                v[i][j] = more[i] && c < E ? part[(size_t)q * E + c] : 0.f;
+            }
         }
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+#pragma unroll
+            for (int j = 0; j < NC; ++j) acc[j] += v[i][j];
+        if (!more[G - 1]) break;
     }
     float* dst = dwte + (size_t)id * E;
 #pragma unroll
@@ -220,18 +248,14 @@ extern "C" size_t ergm_embed_bwd_workspace_size(int T) {
     return keys_bytes(T) + (size_t)3 * T * 1024 * sizeof(float);
 }
 
-extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* dh0,
-                              const float* dcap, float* dwte, float* dwpe, void* ws, size_t ws_bytes, int B, int S, int E,
-                              int V, void* stream) {
-    ERGM_CHECK_ARG(ids && cap_ids && dh0 && dcap && dwte && dwpe, "embed_bwd: null argument");
-    ERGM_CHECK_ARG(B > 0 && S > 0 && E > 0 && E % 4 == 0 && E <= 1024, "embed_bwd: bad shape");
-    const int T = B * S;
+namespace ergm {
+// Sort the lookups of one batch by vocabulary row (only needs the ids: the training executor runs it
+// during the forward, off the critical path) and flag the touched rows.
+int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
+                   uint8_t* row_flag, int n_flag, hipStream_t s) {
+    ERGM_CHECK_ARG(ids && cap_ids && keys, "embed_bwd: null argument");
     ERGM_CHECK_ARG(3 * T <= SORT_MAX, "embed_bwd: 3*B*S=%d exceeds the single-workgroup sort (%d)", 3 * T, SORT_MAX);
-    ERGM_CHECK_ARG(ws && ws_bytes >= ergm_embed_bwd_workspace_size(T), "embed_bwd: workspace too small");
-    ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
-    hipStream_t s = as_stream(stream);
-    uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
-    int npad = next_pow2(3 * T);
+    ERGM_CHECK_ARG(!row_flag || n_flag >= V, "embed_bwd: row_flag shorter than the vocabulary");
     static bool attr_set = false;  // benign race: idempotent attribute write
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)embed_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -239,10 +263,20 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
             return fail(ERGM_EHIP, "embed_bwd: cannot raise dynamic LDS limit");
         attr_set = true;
     }
+    if (row_flag && hipMemsetAsync(row_flag, 0, (size_t)n_flag, s) != hipSuccess)
+        return fail(ERGM_EHIP, "embed_bwd: memset");
+    const int npad = next_pow2(3 * T);
     hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), (size_t)npad * sizeof(uint64_t), s, ids, tt, cap_ids, T,
-                       V, npad, keys);
-    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + keys_bytes(T));
-    const int n = 3 * T;
+                       V, npad, keys, row_flag);
+    return check_launch("embed_bwd_sort");
+}
+
+// dwte[id] += Σ (ordered) of the lookup gradients of each sorted run; dwpe = Σ_b dh0[b].
+// part: 3T x E floats of scratch.
+int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
+                   float* dwpe, float* part, hipStream_t s) {
+    ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
+    const int T = B * S, n = 3 * T;
     dim3 g1(cdiv(n, SEG_CH)), g2(n);
 #define ERGM_SEG(NC)                                                                                         \
     hipLaunchKernelGGL(embed_runsum_kernel<NC>, g1, dim3(256), 0, s, keys, n, T, dh0, dcap, part, E);         \
@@ -257,4 +291,20 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
     ERGM_TRY(check_launch("embed_bwd"));
     // dwpe[s][e] = Σ_b dh0[b][s][e]   (rows b of [B][S*E])
     return colsum_impl(dh0, false, B, S * E, S * E, dwpe, 0, nullptr, 0, s);
+}
+}  // namespace ergm
+
+extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* dh0,
+                              const float* dcap, float* dwte, float* dwpe, void* ws, size_t ws_bytes, int B, int S, int E,
+                              int V, void* stream) {
+    ERGM_CHECK_ARG(ids && cap_ids && dh0 && dcap && dwte && dwpe, "embed_bwd: null argument");
+    ERGM_CHECK_ARG(B > 0 && S > 0 && E > 0 && E % 4 == 0 && E <= 1024, "embed_bwd: bad shape");
+    const int T = B * S;
+    ERGM_CHECK_ARG(ws && ws_bytes >= ergm_embed_bwd_workspace_size(T), "embed_bwd: workspace too small");
+    ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
+    hipStream_t s = as_stream(stream);
+    uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
+    ERGM_TRY(embed_bwd_sort(ids, tt, cap_ids, T, V, keys, nullptr, 0, s));
+    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + keys_bytes(T));
+    return embed_bwd_sums(keys, B, S, E, dh0, dcap, dwte, dwpe, part, s);
 }

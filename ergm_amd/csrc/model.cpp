@@ -34,6 +34,10 @@ int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, i
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
                  int V, hipStream_t s);
+int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
+                   uint8_t* row_flag, int n_flag, hipStream_t s);
+int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
+                   float* dwpe, float* part, hipStream_t s);
 }  // namespace ergm
 
 struct LayerActs {
@@ -60,6 +64,10 @@ struct ergm_model_plan {
     __bf16* dlogits;
     float *row_loss, *emo_sum, *emo_tmp;
     int* n_valid_local;
+    // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
+    // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
+    uint64_t* keys;
+    uint8_t* row_flag;
     // backward scratch
     float *dh, *dy, *dcap, *delta;
     __bf16 *d_o, *dkv_all;
@@ -135,6 +143,7 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->emo_sum = c.take<float>(4);
     P->emo_tmp = c.take<float>((size_t)d.batch * 16 + 8);
     P->n_valid_local = c.take<int>(4);
+    P->keys = c.take<uint64_t>(3 * T);
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
     P->d_o = c.take<__bf16>(T * E);
@@ -349,6 +358,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     }
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
+    P->row_flag = nullptr;
     P->n_valid = nullptr;
     P->B_global = d.batch;
     P->probe = 0;
@@ -374,6 +384,13 @@ extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begi
     P->probe = probe;
     P->ev_begin = reinterpret_cast<hipEvent_t>(ev_begin);
     P->ev_end = reinterpret_cast<hipEvent_t>(ev_end);
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_row_flags(ergm_model_plan* P, void* row_flag, int n) {
+    ERGM_CHECK_ARG(P, "model_set_row_flags: null plan");
+    ERGM_CHECK_ARG(!row_flag || n >= P->d.vocab_pad, "model_set_row_flags: need %d bytes (got %d)", P->d.vocab_pad, n);
+    P->row_flag = reinterpret_cast<uint8_t*>(row_flag);
     return ERGM_OK;
 }
 
@@ -406,6 +423,9 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
+        // the embedding backward's sort needs only the ids: done here, off the critical chain
+        if (train && !P->dry)
+            ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
         Probe pr(P, 4, ss);
         ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
                       ERGM_EPI_BIAS, p.capkv_b));
@@ -588,10 +608,13 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));
     if (P->dry) return ERGM_OK;
-    // every side-stream gradient (incl. the LM-head dwte) is final before the lookup gradients are added
-    ERGM_TRY(join_side(P, s, L + 2));
-    return ergm_embed_bwd(P->ids, P->tt, P->cap_ids, P->dh, P->dcap, p.g_wte, p.g_wpe, P->scratch, P->scratch_bytes,
-                          d.batch, d.seq, E, d.vocab, s);
+    // the LM-head dwte (side stream, marked L+1) is final before the lookup gradients are added to it;
+    // the caption K/V weight gradient keeps running on the side stream meanwhile
+    ERGM_TRY(join_side(P, s, L + 1));
+    ERGM_TRY(ws_need(P, (size_t)3 * T * E * sizeof(float)));
+    ERGM_TRY(embed_bwd_sums(P->keys, d.batch, d.seq, E, P->dh, P->dcap, p.g_wte, p.g_wpe,
+                            reinterpret_cast<float*>(P->scratch), s));
+    return join_side(P, s, L + 2);  // every gradient final on the caller's stream
 }
 
 }  // namespace

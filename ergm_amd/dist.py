@@ -58,6 +58,23 @@ class DPSync:
             self._stream = torch.cuda.Stream(dev)
         return self._stream
 
+    def enqueue(self, grad: torch.Tensor, fn, key: int) -> None:
+        """Run ``fn()`` on the side stream once everything issued so far on the current stream is
+        done (``key`` selects the reusable ordering event; fn launches work, it does not wait)."""
+        if not grad.is_cuda:
+            fn()
+            return
+        cur = torch.cuda.current_stream(grad.device)
+        side = self._side(grad.device)
+        while len(self._events) <= key:
+            from ._lib import HipEvent
+            self._events.append(HipEvent(sync=True))
+        ev = self._events[key]  # reused every step: the wait below is enqueued right after the record
+        ev.record(cur.cuda_stream)
+        ev.wait(side.cuda_stream)
+        with torch.cuda.stream(side):
+            fn()
+
     def bucket_ready(self, k: int, grad: torch.Tensor, post=None) -> None:
         """Bucket k of the flat gradient buffer `grad` is final on the current stream: start its
         all-reduce (SUM) on the side stream, then run ``post(a, b)`` there once the reduced values are
@@ -65,35 +82,18 @@ class DPSync:
         if not self.active and post is None:
             return
         a, b = self.buckets[k]
-        if grad.is_cuda:
-            cur = torch.cuda.current_stream(grad.device)
-            side = self._side(grad.device)
-            while len(self._events) <= k:
-                from ._lib import HipEvent
-                self._events.append(HipEvent(sync=True))
-            ev = self._events[k]  # reused every step: the wait below is enqueued right after the record
-            ev.record(cur.cuda_stream)
-            ev.wait(side.cuda_stream)
-            with torch.cuda.stream(side):
-                if self.active:
-                    import torch.distributed as dist
-                    work = dist.all_reduce(grad[a:b], group=self.pg, async_op=True)
-                    if post is not None:
-                        work.wait()  # side stream waits for the collective; no host synchronisation
-                    else:
-                        self._works.append(work)
-                if post is not None:
-                    post(a, b)
-        else:
+
+        def run():
             if self.active:
                 import torch.distributed as dist
                 work = dist.all_reduce(grad[a:b], group=self.pg, async_op=True)
                 if post is not None:
-                    work.wait()
+                    work.wait()  # the side stream waits for the collective; no host synchronisation
                 else:
                     self._works.append(work)
             if post is not None:
                 post(a, b)
+        self.enqueue(grad, run, k)
 
     def finish(self, grad: torch.Tensor) -> None:
         """Make the current stream wait for every outstanding bucket (no host synchronisation)."""

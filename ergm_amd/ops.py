@@ -180,6 +180,19 @@ def adamw_step(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, ma
            weight_decay, lr / bc1, math.sqrt(bc2), int(max_blocks), _stream(p.device))
 
 
+def adamw_rows(p, g, m, v, p_bf16, row_len, row_flag, select, lr, beta1, beta2, eps, weight_decay, step,
+               max_blocks=0):
+    """``adamw_step`` restricted to rows r of the [numel/row_len, row_len] block with
+    (row_flag[r] != 0) == select (row_flag: a uint8 tensor or a raw device pointer)."""
+    import math
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    rows = p.numel() // row_len
+    flag = C.c_void_p(row_flag) if isinstance(row_flag, int) else _ptr(row_flag)
+    L.call("ergm_adamw_rows", _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), rows, row_len, flag, int(select), lr,
+           beta1, beta2, eps, weight_decay, lr / bc1, math.sqrt(bc2), int(max_blocks), _stream(p.device))
+
+
 def cast_bf16(src, dst):
     L.call("ergm_cast_bf16", _ptr(src), _ptr(dst), src.numel(), _stream(src.device))
 

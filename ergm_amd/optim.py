@@ -73,8 +73,13 @@ class FusedAdamW(torch.optim.Optimizer):
         self._applied.add(id(flat))
         nb = self.overlap_blocks
 
-        def post(a, b):
-            ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t, nb)
+        def post(a, b, rows=None):
+            if rows is None:
+                ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t, nb)
+            else:  # (row_len, row_flag, select): only the selected rows of the [.., row_len] block
+                row_len, flags, select = rows
+                ops.adamw_rows(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], row_len, flags, select, lr, b1,
+                               b2, eps, wd, t, nb)
         return post
 
     @torch.no_grad()

@@ -107,10 +107,12 @@ def build_layout(vocab: int, E: int, L: int, F: int, P: int, num_emotions: int =
     views["__capkv_w"] = View(capw, (E, L * 2 * E), (L * 2 * E, 1))
     views["__capkv_b"] = View(capb, (L * 2 * E,), (1,))
     put("transformer.wpe.weight", (P, E))
+    seg["capwpe"] = (s0, off)
     wte_off = off
     views["transformer.wte.weight"] = View(wte_off, (vocab, E), (E, 1))
     views["__wte_pad"] = View(wte_off, (vocab_pad, E), (E, 1))
     off = _al(off + vocab_pad * E)
+    seg["wte"] = (wte_off, off)
     seg["embed"] = (s0, off)
     return Layout(vocab, vocab_pad, E, L, F, P, off, views, layer_base, layer_stride, layer_off, seg)
 

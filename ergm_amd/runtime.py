@@ -75,6 +75,10 @@ class ModelRunner:
         self.dp = DPSync(process_group, dp_buckets(layout))
         self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)
         self._inputs = None
+        # rows of the tied wte the batch's lookups touch (written by every training forward)
+        self.row_flags = torch.zeros(layout.vocab_pad, dtype=torch.uint8, device=self.dev)
+        L.check(self.lib.ergm_model_set_row_flags(self.plan, _p(self.row_flags), layout.vocab_pad),
+                "ergm_model_set_row_flags")
 
     def __del__(self):
         try:
@@ -109,18 +113,38 @@ class ModelRunner:
     # ---- backward -----------------------------------------------------------------------
     def backward(self, grad_scale: Optional[torch.Tensor], post=None) -> None:
         """Writes every parameter gradient into self.grad (overwrite, not accumulate).  With a
-        process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final."""
+        process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final.
+
+        ``post(a, b, rows=None)`` (the overlapped optimizer) is run on that side stream for each final
+        range.  Single-process, the tied wte is updated in two parts: the rows no lookup of this batch
+        touched are final with the LM-head weight gradient (after block L-2's stage) and are updated
+        while the remaining blocks are differentiated; the touched rows follow the embedding backward."""
         s = self._stream()
         lib = self.lib
         self.dp.begin()
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
-        Lyr = self.layout.L
+        Lyr, E = self.layout.L, self.layout.E
+        split_wte = post is not None and not self.dp.active
+        wa, wb = self.layout.seg["wte"]
+        ka = Lyr + 1  # ordering-event keys beyond the buckets'
+
+        def wte_rows(select):
+            return lambda: post(wa, wb, rows=(E, self.row_flags, select))
         # bucket i = (head +) block L-1-i; its weight gradients are joined one stage later (ergm_hip.h)
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
             if i >= 1:
                 self.dp.bucket_ready(i - 1, self.grad, post)
+            if split_wte and i == 1:
+                self.dp.enqueue(self.grad, wte_rows(0), ka)
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
         self.dp.bucket_ready(Lyr - 1, self.grad, post)
-        self.dp.bucket_ready(Lyr, self.grad, post)
+        if split_wte:
+            ca, cb = self.layout.seg["capwpe"]
+            if Lyr == 1:
+                self.dp.enqueue(self.grad, wte_rows(0), ka)
+            self.dp.enqueue(self.grad, lambda: post(ca, cb), ka + 1)
+            self.dp.enqueue(self.grad, wte_rows(1), ka + 2)
+        else:
+            self.dp.bucket_ready(Lyr, self.grad, post)
         self.dp.finish(self.grad)

@@ -173,6 +173,13 @@ int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
 int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
                     float beta1, float beta2, float eps, float weight_decay, float step_size,
                     float bc2_sqrt, int max_blocks, void* stream);
+/* The same update restricted to the rows of a [rows][row_len] block whose flag byte matches:
+ * row r is updated iff (row_flag[r] != 0) == (select != 0).  With ergm_model_set_row_flags this
+ * splits the tied-embedding update into the rows only the LM head touched (final early in the
+ * backward) and the rows the lookups touched (final after the embedding backward). */
+int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
+                    const void* row_flag, int select, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream);
 /* bf16 shadow copy of fp32 values: dst[i] = bf16(src[i]). */
 int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream);
 /* y[i] += x[i] (f32), used to accumulate gradients across backward calls. */
@@ -226,6 +233,13 @@ int ergm_model_destroy(ergm_model_plan* plan);
 /* Inputs for the next forward (device pointers, int64 [B][S]; features f32 or NULL; labels may be
  * NULL for inference).  n_valid_global: device int the caller filled (ergm_count_valid +
  * optional all-reduce); B_global: global batch for the emotion-loss mean.                       */
+/* Optional: a caller-owned byte per padded vocabulary row (n >= vocab_pad).  When set, every training
+ * forward writes 1 for the rows its token / token-type / caption lookups touch and 0 elsewhere
+ * (stream-ordered, final once the forward returns on its stream).  The lookup gradients of the
+ * embedding backward land only in flagged rows of g_wte; all other rows of g_wte are final once
+ * the LM-head weight gradient is (after ergm_model_backward_layer(L-2)), which lets an optimizer
+ * update them while the rest of the backward runs.  NULL disables. */
+int ergm_model_set_row_flags(ergm_model_plan* plan, void* row_flag, int n);
 int ergm_model_set_inputs(ergm_model_plan* plan, const int64_t* ids, const int64_t* tt,
                           const int64_t* cap_ids, const float* vis, const float* aud,
                           const int64_t* labels, const int64_t* emotion_labels,

@@ -137,11 +137,13 @@ def test_adamw_step_and_loss_decrease(gpu):
     assert losses[-1] < losses[0] - 0.05, losses
 
 
-def test_overlapped_adamw_matches_step_adamw(gpu):
-    """FusedAdamW(overlap=True) applies the same per-bucket update during backward: bitwise equal
-    parameters, moments and bf16 shadow to the plain step() path over a scheduled LR."""
+@pytest.mark.parametrize("name", ["tiny_e64.npz", "small_e128_v500.npz"])
+def test_overlapped_adamw_matches_step_adamw(gpu, name):
+    """FusedAdamW(overlap=True) applies the same update during backward — per gradient bucket, the
+    tied wte split into untouched / lookup-touched rows — bitwise equal parameters, moments and bf16
+    shadow to the plain step() path over a scheduled LR."""
     from ergm_amd.optim import get_polynomial_decay_schedule_with_warmup
-    rec = _load("small_e128_v500.npz")
+    rec = _load(name)
     runs = []
     for overlap in (False, True):
         _, _, _, model, batch = _setup(rec, gpu)

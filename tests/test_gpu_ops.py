@@ -319,3 +319,26 @@ def test_adamw_matches_oracle(gpu):
         ops.adamw_step(p, G.to(gpu), m, v, pb, lr, 0.9, 0.999, 1e-8, 0.01, i + 1)
     assert torch.allclose(p.cpu(), P["x"], rtol=2e-6, atol=1e-7)
     assert torch.equal(pb.cpu(), p.cpu().bfloat16())
+
+
+def test_adamw_rows_partition_equals_full_update(gpu):
+    """The two row-selective passes (flag 0 rows, then flag 1 rows) are bitwise the full update; a
+    capped grid (grid-stride loops) changes nothing."""
+    rows, E = 300, 96
+    torch.manual_seed(5)
+    p0, g = torch.randn(rows * E, device=gpu), torch.randn(rows * E, device=gpu)
+    m0, v0 = torch.randn(rows * E, device=gpu) * 0.1, torch.rand(rows * E, device=gpu) * 0.01
+    flags = (torch.rand(rows, device=gpu) < 0.3).to(torch.uint8)
+    ref = [t.clone() for t in (p0, m0, v0)]
+    pb_ref = torch.empty(rows * E, dtype=torch.bfloat16, device=gpu)
+    ops.adamw_step(ref[0], g, ref[1], ref[2], pb_ref, 1e-3, 0.9, 0.999, 1e-8, 0.01, 7)
+    for cap in (0, 3):
+        got = [t.clone() for t in (p0, m0, v0)]
+        pb = torch.zeros(rows * E, dtype=torch.bfloat16, device=gpu)
+        ops.adamw_rows(got[0], g, got[1], got[2], pb, E, flags, 0, 1e-3, 0.9, 0.999, 1e-8, 0.01, 7, cap)
+        sel = flags.bool().repeat_interleave(E)
+        assert torch.equal(got[0][sel], p0[sel])  # flagged rows untouched by the select-0 pass
+        ops.adamw_rows(got[0], g, got[1], got[2], pb, E, flags, 1, 1e-3, 0.9, 0.999, 1e-8, 0.01, 7, cap)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
+        assert torch.equal(pb, pb_ref)
