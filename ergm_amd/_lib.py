@@ -80,6 +80,9 @@ _SIGS = {
     "ergm_model_destroy": (i32, [vp]),
     "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
     "ergm_model_set_row_flags": (i32, [vp, vp, i32]),
+    "ergm_model_set_lookup_compact": (i32, [vp, vp, vp]),
+    "ergm_rows_scan": (i32, [vp, i32, vp, vp, vp]),
+    "ergm_rows_compact": (i32, [vp, vp, i32, i32, vp, vp, i32, vp]),
     "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
     "ergm_model_forward": (i32, [vp, vp, vp, vp, i32, vp]),
     "ergm_model_backward_head": (i32, [vp, vp, vp]),

@@ -9,6 +9,8 @@
 // atomics (the token-type rows would otherwise take ~B·S/2 colliding adds each).
 #include "common.h"
 
+#include <algorithm>
+
 namespace ergm {
 
 template <int NV>
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void embed_runsum_kernel(const uint64_t* __res
 template <int NC>
 __global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __restrict__ keys, int n,
                                                            const float* __restrict__ part, float* __restrict__ dwte,
-                                                           int E) {
+                                                           const int* __restrict__ row_pos, int E) {
     const int p = blockIdx.x;
     const uint64_t k = keys[p];
     if (k == ~0ull) return;
@@ -191,11 +193,61 @@ __global__ __launch_bounds__(256) void embed_segsum_kernel(const uint64_t* __res
             for (int j = 0; j < NC; ++j) acc[j] += v[i][j];
         if (!more[G - 1]) break;
     }
-    float* dst = dwte + (size_t)id * E;
+    // dense: accumulate into dwte[id]; compact (row_pos given): the zeroed slot row_pos[id] of dwte
+    float* dst = dwte + (size_t)(row_pos ? row_pos[id] : id) * E;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
         int c = threadIdx.x + j * 256;
         if (c < E) dst[c] += acc[j];
+    }
+}
+
+// ---- compact lookup rows (data parallelism) ------------------------------------------------------
+// The lookup part of the tied-wte gradient lives in the rows the batch touched.  Under data
+// parallelism the union of those rows over all ranks (flags all-reduced with MAX) is numbered by an
+// exclusive prefix sum, the lookup sums go to compact[pos[row]], and only that compact block is
+// all-reduced and added back — instead of a second all-reduce of the whole [V, E] gradient.
+
+// pos[r] = number of flagged rows before r; count[0] = total.  One workgroup (n <= 1024 * 1024).
+__global__ __launch_bounds__(1024) void rows_scan_kernel(const uint8_t* __restrict__ flag, int n, int* __restrict__ pos,
+                                                         int* __restrict__ count) {
+    __shared__ int part[1024];
+    const int per = (n + 1023) / 1024;
+    const int r0 = threadIdx.x * per, r1 = min(n, r0 + per);
+    int c = 0;
+    for (int r = r0; r < r1; ++r) c += flag[r] != 0;
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+        int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (int r = r0; r < r1; ++r) {
+        pos[r] = run;
+        run += flag[r] != 0;
+    }
+    if (threadIdx.x == 1023) count[0] = part[1023];
+}
+
+// mode 0: compact[pos[r]] = 0;  mode 1: dst[r] += compact[pos[r]]   (flagged rows r only)
+__global__ __launch_bounds__(256) void rows_compact_kernel(const uint8_t* __restrict__ flag, const int* __restrict__ pos,
+                                                           int n, int row4, float4* __restrict__ compact,
+                                                           float4* __restrict__ dst, int mode) {
+    for (int r = blockIdx.x; r < n; r += gridDim.x) {
+        if (!flag[r]) continue;
+        float4* c = compact + (size_t)pos[r] * row4;
+        for (int j = threadIdx.x; j < row4; j += 256) {
+            if (mode == 0) {
+                c[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float4 a = dst[(size_t)r * row4 + j], b = c[j];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+                dst[(size_t)r * row4 + j] = a;
+            }
+        }
     }
 }
 
@@ -274,13 +326,13 @@ int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
 // dwte[id] += Σ (ordered) of the lookup gradients of each sorted run; dwpe = Σ_b dh0[b].
 // part: 3T x E floats of scratch.
 int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
-                   float* dwpe, float* part, hipStream_t s) {
+                   float* dwpe, float* part, const int* row_pos, hipStream_t s) {
     ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
     const int T = B * S, n = 3 * T;
     dim3 g1(cdiv(n, SEG_CH)), g2(n);
 #define ERGM_SEG(NC)                                                                                         \
     hipLaunchKernelGGL(embed_runsum_kernel<NC>, g1, dim3(256), 0, s, keys, n, T, dh0, dcap, part, E);         \
-    hipLaunchKernelGGL(embed_segsum_kernel<NC>, g2, dim3(256), 0, s, keys, n, part, dwte, E);
+    hipLaunchKernelGGL(embed_segsum_kernel<NC>, g2, dim3(256), 0, s, keys, n, part, dwte, row_pos, E);
     switch (cdiv(E, 256)) {
         case 1: ERGM_SEG(1) break;
         case 2: ERGM_SEG(2) break;
@@ -306,5 +358,22 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
     uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
     ERGM_TRY(embed_bwd_sort(ids, tt, cap_ids, T, V, keys, nullptr, 0, s));
     float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + keys_bytes(T));
-    return embed_bwd_sums(keys, B, S, E, dh0, dcap, dwte, dwpe, part, s);
+    return embed_bwd_sums(keys, B, S, E, dh0, dcap, dwte, dwpe, part, nullptr, s);
+}
+
+extern "C" int ergm_rows_scan(const void* row_flag, int n, int* pos, int* count, void* stream) {
+    ERGM_CHECK_ARG(row_flag && pos && count && n > 0 && n <= 1024 * 1024, "rows_scan: bad argument");
+    hipLaunchKernelGGL(rows_scan_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (const uint8_t*)row_flag, n, pos,
+                       count);
+    return check_launch("rows_scan");
+}
+
+extern "C" int ergm_rows_compact(const void* row_flag, const int* pos, int n, int row_len, float* compact, float* dst,
+                                 int mode, void* stream) {
+    ERGM_CHECK_ARG(row_flag && pos && compact && n > 0 && row_len > 0 && row_len % 4 == 0, "rows_compact: bad argument");
+    ERGM_CHECK_ARG(mode == 0 || (mode == 1 && dst), "rows_compact: mode 0 (zero) or 1 (scatter-add into dst)");
+    ERGM_CHECK_ARG(aligned16(compact) && (!dst || aligned16(dst)), "rows_compact: 16-byte alignment");
+    hipLaunchKernelGGL(rows_compact_kernel, dim3(std::min(n, 8192)), dim3(256), 0, as_stream(stream),
+                       (const uint8_t*)row_flag, pos, n, row_len / 4, (float4*)compact, (float4*)dst, mode);
+    return check_launch("rows_compact");
 }

@@ -37,7 +37,7 @@ int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, 
 int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
                    uint8_t* row_flag, int n_flag, hipStream_t s);
 int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
-                   float* dwpe, float* part, hipStream_t s);
+                   float* dwpe, float* part, const int* row_pos, hipStream_t s);
 }  // namespace ergm
 
 struct LayerActs {
@@ -68,6 +68,9 @@ struct ergm_model_plan {
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
     uint8_t* row_flag;
+    // optional compact destination of the lookup gradient sums (data parallelism, ergm_hip.h)
+    const int* row_pos;
+    float* lookup_compact;
     // backward scratch
     float *dh, *dy, *dcap, *delta;
     __bf16 *d_o, *dkv_all;
@@ -359,6 +362,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
     P->row_flag = nullptr;
+    P->row_pos = nullptr;
+    P->lookup_compact = nullptr;
     P->n_valid = nullptr;
     P->B_global = d.batch;
     P->probe = 0;
@@ -391,6 +396,14 @@ extern "C" int ergm_model_set_row_flags(ergm_model_plan* P, void* row_flag, int 
     ERGM_CHECK_ARG(P, "model_set_row_flags: null plan");
     ERGM_CHECK_ARG(!row_flag || n >= P->d.vocab_pad, "model_set_row_flags: need %d bytes (got %d)", P->d.vocab_pad, n);
     P->row_flag = reinterpret_cast<uint8_t*>(row_flag);
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_lookup_compact(ergm_model_plan* P, const int* row_pos, float* compact) {
+    ERGM_CHECK_ARG(P, "model_set_lookup_compact: null plan");
+    ERGM_CHECK_ARG((row_pos == nullptr) == (compact == nullptr), "model_set_lookup_compact: both or neither");
+    P->row_pos = row_pos;
+    P->lookup_compact = compact;
     return ERGM_OK;
 }
 
@@ -612,8 +625,9 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     // the caption K/V weight gradient keeps running on the side stream meanwhile
     ERGM_TRY(join_side(P, s, L + 1));
     ERGM_TRY(ws_need(P, (size_t)3 * T * E * sizeof(float)));
-    ERGM_TRY(embed_bwd_sums(P->keys, d.batch, d.seq, E, P->dh, P->dcap, p.g_wte, p.g_wpe,
-                            reinterpret_cast<float*>(P->scratch), s));
+    ERGM_TRY(embed_bwd_sums(P->keys, d.batch, d.seq, E, P->dh, P->dcap,
+                            P->lookup_compact ? P->lookup_compact : p.g_wte, p.g_wpe,
+                            reinterpret_cast<float*>(P->scratch), P->lookup_compact ? P->row_pos : nullptr, s));
     return join_side(P, s, L + 2);  // every gradient final on the caller's stream
 }
 

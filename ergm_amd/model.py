@@ -127,6 +127,7 @@ class GPT2LMHeadModel(nn.Module):
         self._runners: Dict[tuple, ModelRunner] = {}
         self._b16_version = -1
         self._overlap_opt = None
+        self._force_compact_lookup = False  # tests: the data-parallel wte path in one process
         self.process_group = process_group
         self.init_weights()
 
@@ -212,6 +213,8 @@ class GPT2LMHeadModel(nn.Module):
         if r is None:
             r = ModelRunner(self.layout, self.config, self.flat.data, self.flat_b16, self.grad_buf, B, S, vis_rows,
                             has_feat, self.process_group)
+            if self._force_compact_lookup:
+                r.force_compact_lookup()
             self._runners[key] = r
         return r
 

@@ -79,6 +79,52 @@ class ModelRunner:
         self.row_flags = torch.zeros(layout.vocab_pad, dtype=torch.uint8, device=self.dev)
         L.check(self.lib.ergm_model_set_row_flags(self.plan, _p(self.row_flags), layout.vocab_pad),
                 "ergm_model_set_row_flags")
+        # Data parallelism: the lookup part of the wte gradient is exchanged as a compact block of the
+        # ranks' union of touched rows (ergm_model_set_lookup_compact); the dense LM-head part is
+        # all-reduced early, during the block backward.  compact_lookup can be forced for testing.
+        self.compact_lookup = self.dp.active
+        self._compact_ready = False
+        if self.compact_lookup:
+            self._setup_compact()
+
+    def _setup_compact(self):
+        Vp, E = self.layout.vocab_pad, self.layout.E
+        cap = min(Vp, self.dp.world * 3 * self.B * self.S)
+        self.row_pos = torch.zeros(Vp, dtype=torch.int32, device=self.dev)
+        self.row_count = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.row_count_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.compact = torch.zeros(cap * E, dtype=torch.float32, device=self.dev)
+        self._ev_count = torch.cuda.Event()
+        self._ev_zero = L.HipEvent(sync=True)
+        L.check(self.lib.ergm_model_set_lookup_compact(self.plan, _p(self.row_pos), _p(self.compact)),
+                "ergm_model_set_lookup_compact")
+
+    def force_compact_lookup(self):
+        """Use the data-parallel compact lookup-gradient path even in one process (tests)."""
+        if not self.compact_lookup:
+            self.compact_lookup = True
+            self._setup_compact()
+
+    def _prepare_compact(self):
+        """After a training forward (comm stream): union of touched rows over ranks, their numbering,
+        the count (copied to the host, read at the end of the backward) and zeroed compact rows."""
+        Vp, E, lib = self.layout.vocab_pad, self.layout.E, self.lib
+        dp = self.dp
+
+        def prep():
+            st = torch.cuda.current_stream(self.dev).cuda_stream
+            if dp.active:
+                import torch.distributed as dist
+                dist.all_reduce(self.row_flags, op=dist.ReduceOp.MAX, group=dp.pg, async_op=True).wait()
+            L.check(lib.ergm_rows_scan(_p(self.row_flags), Vp, _p(self.row_pos), _p(self.row_count),
+                                       C.c_void_p(st)), "ergm_rows_scan")
+            self.row_count_host.copy_(self.row_count, non_blocking=True)
+            self._ev_count.record()
+            L.check(lib.ergm_rows_compact(_p(self.row_flags), _p(self.row_pos), Vp, E, _p(self.compact), None, 0,
+                                          C.c_void_p(st)), "ergm_rows_compact")
+            self._ev_zero.record(st)
+        dp.enqueue(self.grad, prep, self.layout.L + 4)
+        self._compact_ready = True
 
     def __del__(self):
         try:
@@ -108,6 +154,8 @@ class ModelRunner:
         loss = torch.empty(3, dtype=torch.float32, device=dev) if (labels is not None or emo_labels is not None) else None
         L.check(self.lib.ergm_model_forward(self.plan, _p(logits), _p(emo), _p(loss), int(train), s),
                 "ergm_model_forward")
+        if train and self.compact_lookup:
+            self._prepare_compact()
         return logits, emo, loss
 
     # ---- backward -----------------------------------------------------------------------
@@ -121,30 +169,65 @@ class ModelRunner:
         while the remaining blocks are differentiated; the touched rows follow the embedding backward."""
         s = self._stream()
         lib = self.lib
-        self.dp.begin()
+        dp = self.dp
+        dp.begin()
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
-        Lyr, E = self.layout.L, self.layout.E
-        split_wte = post is not None and not self.dp.active
+        Lyr, E, Vp = self.layout.L, self.layout.E, self.layout.vocab_pad
+        compact = self.compact_lookup
+        if compact and not self._compact_ready:
+            raise RuntimeError("backward without a training forward")
+        split_wte = compact or (post is not None and not dp.active)
         wa, wb = self.layout.seg["wte"]
+        ca, cb = self.layout.seg["capwpe"]
         ka = Lyr + 1  # ordering-event keys beyond the buckets'
 
-        def wte_rows(select):
-            return lambda: post(wa, wb, rows=(E, self.row_flags, select))
+        def reduce(a, b):
+            if dp.active:
+                import torch.distributed as dist
+                dist.all_reduce(self.grad[a:b], group=dp.pg, async_op=True).wait()
+
+        def wte_lm_rows():  # dense LM-head part of g_wte (all rows), then the untouched rows' update
+            if compact:
+                reduce(wa, wb)
+            if post is not None:
+                post(wa, wb, rows=(E, self.row_flags, 0))
+
+        def capwpe():
+            if compact:
+                reduce(ca, cb)
+            if post is not None:
+                post(ca, cb)
+
+        def wte_lookup_rows():  # lookup part of the touched rows, then their update
+            if compact:
+                self._ev_count.synchronize()  # recorded right after the forward: long complete
+                n = int(self.row_count_host[0]) * E
+                if dp.active and n:
+                    import torch.distributed as dist
+                    dist.all_reduce(self.compact[:n], group=dp.pg, async_op=True).wait()
+                st = torch.cuda.current_stream(self.dev).cuda_stream
+                L.check(lib.ergm_rows_compact(_p(self.row_flags), _p(self.row_pos), Vp, E, _p(self.compact),
+                                              C.c_void_p(self.grad.data_ptr() + 4 * wa), 1, C.c_void_p(st)),
+                        "ergm_rows_compact")
+            if post is not None:
+                post(wa, wb, rows=(E, self.row_flags, 1))
         # bucket i = (head +) block L-1-i; its weight gradients are joined one stage later (ergm_hip.h)
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
             if i >= 1:
-                self.dp.bucket_ready(i - 1, self.grad, post)
+                dp.bucket_ready(i - 1, self.grad, post)
             if split_wte and i == 1:
-                self.dp.enqueue(self.grad, wte_rows(0), ka)
+                dp.enqueue(self.grad, wte_lm_rows, ka)
+        if compact:
+            self._ev_zero.wait(s.value)  # compact rows zeroed before the lookup sums land in them
+            self._compact_ready = False
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
-        self.dp.bucket_ready(Lyr - 1, self.grad, post)
+        dp.bucket_ready(Lyr - 1, self.grad, post)
         if split_wte:
-            ca, cb = self.layout.seg["capwpe"]
             if Lyr == 1:
-                self.dp.enqueue(self.grad, wte_rows(0), ka)
-            self.dp.enqueue(self.grad, lambda: post(ca, cb), ka + 1)
-            self.dp.enqueue(self.grad, wte_rows(1), ka + 2)
+                dp.enqueue(self.grad, wte_lm_rows, ka)
+            dp.enqueue(self.grad, capwpe, ka + 1)
+            dp.enqueue(self.grad, wte_lookup_rows, ka + 2)
         else:
-            self.dp.bucket_ready(Lyr, self.grad, post)
-        self.dp.finish(self.grad)
+            dp.bucket_ready(Lyr, self.grad, post)
+        dp.finish(self.grad)

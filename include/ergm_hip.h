@@ -240,6 +240,16 @@ int ergm_model_destroy(ergm_model_plan* plan);
  * the LM-head weight gradient is (after ergm_model_backward_layer(L-2)), which lets an optimizer
  * update them while the rest of the backward runs.  NULL disables. */
 int ergm_model_set_row_flags(ergm_model_plan* plan, void* row_flag, int n);
+/* Optional (data parallelism): route the lookup gradient sums of the embedding backward to
+ * compact[row_pos[row]] (rows of E floats, added onto caller-zeroed rows) instead of adding them to
+ * g_wte[row].  row_pos = ergm_rows_scan of the rank-union of the row flags.  NULLs disable. */
+int ergm_model_set_lookup_compact(ergm_model_plan* plan, const int* row_pos, float* compact);
+/* pos[r] = number of nonzero flags before r (exclusive prefix sum), count[0] = the total. */
+int ergm_rows_scan(const void* row_flag, int n, int* pos, int* count, void* stream);
+/* For every flagged row r of n: mode 0 zeroes compact[pos[r]]; mode 1 adds it into dst[r]
+ * (rows of row_len floats). */
+int ergm_rows_compact(const void* row_flag, const int* pos, int n, int row_len, float* compact, float* dst,
+                      int mode, void* stream);
 int ergm_model_set_inputs(ergm_model_plan* plan, const int64_t* ids, const int64_t* tt,
                           const int64_t* cap_ids, const float* vis, const float* aud,
                           const int64_t* labels, const int64_t* emotion_labels,

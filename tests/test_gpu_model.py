@@ -164,6 +164,28 @@ def test_overlapped_adamw_matches_step_adamw(gpu, name):
     assert a[4] == b[4] == 3.0 and a[5] == b[5]
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+def test_compact_lookup_path_matches_dense(gpu, overlap):
+    """The data-parallel exchange of the wte lookup gradient (union row flags, prefix-sum numbering,
+    compact block, scatter-add) run in one process gives bitwise the dense path's gradients and, with
+    the overlapped optimizer, the same parameters."""
+    rec = _load("small_e128_v500.npz")
+    runs = []
+    for compact in (False, True):
+        _, _, _, model, batch = _setup(rec, gpu)
+        model._force_compact_lookup = compact
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=overlap)
+        for _ in range(2):
+            opt.zero_grad()
+            _run(model, batch, gpu)
+            g = model.flat.grad.clone()
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append((g, model.flat.detach().clone(), model.flat_b16.clone()))
+    for x, y in zip(*runs):
+        assert torch.equal(x, y)
+
+
 def test_backward_is_deterministic(gpu):
     rec = _load("small_e128_v500.npz")
     _, _, _, model, batch = _setup(rec, gpu)
