@@ -516,7 +516,6 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 6},    // 13
     {128, 128, 2, 2, 4},   // 14
     {128, 128, 4, 2, 4},   // 15 8 waves
-    {256, 128, 4, 2, 4},   // 16 8 waves, 144 KiB
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -616,8 +615,7 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 12: launch_pipe_cfg<12, AKM, BKN, EPI, OB>(a, split, s); break;
         case 13: launch_pipe_cfg<13, AKM, BKN, EPI, OB>(a, split, s); break;
         case 14: launch_pipe_cfg<14, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 15: launch_pipe_cfg<15, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<16, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<15, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 

@@ -31,6 +31,8 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s);
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
+int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
+                             float* const* dgamma, float* const* dbeta, hipStream_t s);
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
                  int V, hipStream_t s);
@@ -80,6 +82,11 @@ struct ergm_model_plan {
     // dγ/dβ partials of each LayerNorm backward (one slot per LN, reduced on the side stream)
     std::vector<float*> ln_part;
     int ln_slot;
+    int ln_pending;  // LayerNorm backwards whose dγ/dβ reduction is not yet launched (ln_reduce_flush)
+    const float* lnr_pg[4];
+    const float* lnr_pb[4];
+    float* lnr_dg[4];
+    float* lnr_db[4];
     char *scratch, *scratch2;
     size_t scratch_bytes;
     // Two HIP streams: the caller's stream runs the critical chain; `side` runs weight-gradient GEMMs
@@ -234,8 +241,9 @@ int dw_gemm(ergm_model_plan* P, hipStream_t s_main, int M, int N, const __bf16* 
     return colsum(P, s, dY, ERGM_BF16, T, N, ldy, gB);
 }
 
-// LayerNorm backward on the critical chain; its dγ/dβ partial reduction is forked to the side stream
-// (partials live in a per-LN slot, so nothing later overwrites them before the reduce runs).
+// LayerNorm backward on the critical chain; its dγ/dβ partials go to a per-LN slot (nothing later
+// overwrites them) and are reduced on the side stream: by ln_reduce_flush, which batches the pending
+// LayerNorms of a block into one launch.
 int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
            float* dgamma, float* dbeta, __bf16* dh_b, int slot) {
     if (P->dry) return ERGM_OK;
@@ -243,8 +251,18 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
     float* pg = P->ln_part[slot];
     float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
     ERGM_TRY(layernorm_bwd_main(P->dy, x, mean, rstd, gamma, P->dh, dh_b, pg, pb, T, E, s));
+    ERGM_CHECK_ARG(P->ln_pending < 4, "model: too many pending LayerNorm reductions");
+    const int k = P->ln_pending++;
+    P->lnr_pg[k] = pg; P->lnr_pb[k] = pb; P->lnr_dg[k] = dgamma; P->lnr_db[k] = dbeta;
+    return ERGM_OK;
+}
+
+int ln_reduce_flush(ergm_model_plan* P, hipStream_t s) {
+    if (P->dry || P->ln_pending == 0) return ERGM_OK;
     ERGM_TRY(fork_side(P, s));
-    return layernorm_param_reduce(pg, pb, T, E, dgamma, dbeta, P->side);
+    const int n = P->ln_pending;
+    P->ln_pending = 0;
+    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
 }
 
 struct Probe {  // records the probe events around one launch when `id` is the active probe
@@ -334,6 +352,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->dry = false;
     P->need = 0;
     P->have_fwd = false;
+    P->ln_pending = 0;
     // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py
     // lays the flat buffers out that way); otherwise fall back to separate column sums.
     {
@@ -523,6 +542,7 @@ namespace {
 
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     const ergm_model_dims& d = P->d;
+    P->ln_pending = 0;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad, L = d.n_layer;
     // dh_f = dlogits · wte (contraction over the padded vocab) on the main chain; the tied-weight
@@ -606,6 +626,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                     3 * l));
     // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
     // those of the block differentiated before, so block l+1's gradients are final on return.
+    ERGM_TRY(ln_reduce_flush(P, s));  // this block's three LayerNorms (+ ln_f after the head stage)
     ERGM_TRY(side_mark(P, l));
     if (l + 1 < L) ERGM_TRY(join_side(P, s, l + 1));
     return ERGM_OK;

@@ -10,6 +10,7 @@
 namespace ergm {
 
 constexpr int LN_ROWS_PER_BLOCK_BWD = 8;
+constexpr int LN_WAVES_BWD = 8;  // one row per wave: 8 waves per CU in flight at T = 2048
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
@@ -20,14 +21,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;
     const float* xr = x + (size_t)row * E;
-    float4 v[NV];
+    float4 v[NV], gv[NV], bv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {  // every load issued before the first reduction
+        int c = (i * 64 + lane) * 4;
+        const bool in = c < E;
+        v[i] = in ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0, 0, 0, 0);
+        gv[i] = in ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0, 0, 0, 0);
+        bv[i] = in ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0, 0, 0, 0);
+    }
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = (i * 64 + lane) * 4;
-        v[i] = c < E ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0, 0, 0, 0);
-        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    }
+    for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     const float inv_e = 1.0f / (float)E;
     const float mean = wave_sum(s) * inv_e;
     float q = 0.f;
@@ -45,8 +50,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     for (int i = 0; i < NV; ++i) {
         int c = (i * 64 + lane) * 4;
         if (c < E) {
-            float4 g = *reinterpret_cast<const float4*>(gamma + c);
-            float4 b = *reinterpret_cast<const float4*>(beta + c);
+            const float4 g = gv[i], b = bv[i];
             bf16x4 o;
             o[0] = f2bf((v[i].x - mean) * rstd * g.x + b.x);
             o[1] = f2bf((v[i].y - mean) * rstd * g.y + b.y);
@@ -63,12 +67,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 
 // dx = rstd·(g − mean(g) − x̂·mean(g·x̂)), g = dy·γ;  dres += dx;  partial dγ = Σ dy·x̂, dβ = Σ dy
 template <int NV>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+__global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
                                                      float* __restrict__ part_b, int rows, int E) {
-    __shared__ float red[2][4][NV * 256];
+    __shared__ float red[2][LN_WAVES_BWD][NV * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 pg[NV], pb[NV], gm[NV];
 #pragma unroll
@@ -79,9 +83,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
         gm[i] = c < E ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0, 0, 0, 0);
     }
     const float inv_e = 1.0f / (float)E;
-    // each wave owns RPW = LN_ROWS_PER_BLOCK_BWD/4 rows and issues every load of all of them (x, dy and
-    // the residual gradient it adds into) before the first reduction, so the HBM latency is paid once
-    constexpr int RPW = LN_ROWS_PER_BLOCK_BWD / 4;
+    // each wave owns RPW rows and issues every load of all of them (x, dy and the residual gradient it
+    // adds into) before the first reduction, so the HBM latency is paid once
+    constexpr int RPW = LN_ROWS_PER_BLOCK_BWD / LN_WAVES_BWD;
     const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD + wave * RPW;
     float4 xh[RPW][NV], d[RPW][NV], o[RPW][NV];
     float mu[RPW], rs[RPW];
@@ -150,37 +154,60 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
         *reinterpret_cast<float4*>(&red[1][wave][c]) = pb[i];
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < E; c += 256) {
-        float a = ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
-        float b = ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+    for (int c = threadIdx.x; c < E; c += 64 * LN_WAVES_BWD) {
+        float a = red[0][0][c], b = red[1][0][c];
+#pragma unroll
+        for (int w = 1; w < LN_WAVES_BWD; ++w) {
+            a += red[0][w][c];
+            b += red[1][w][c];
+        }
         part_g[(size_t)blockIdx.x * E + c] = a;
         part_b[(size_t)blockIdx.x * E + c] = b;
     }
 }
 
-// dγ / dβ: sum the per-block partials (fixed order).  grid (cdiv(E,64), 2): 64 columns x 4 row lanes.
-__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ part_g,
-                                                              const float* __restrict__ part_b, int nparts, int E,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    __shared__ float red[4][64];
-    const float* part = blockIdx.y == 0 ? part_g : part_b;
-    float* out = blockIdx.y == 0 ? dgamma : dbeta;
+// dγ / dβ: sum the per-block partials (fixed order).  grid (cdiv(E,64), 2), 1024 threads: 64 columns x
+// 16 row lanes, each lane with 16 partial rows in flight per round (one HBM latency per 256 partials).
+struct LnReduceJobs {  // up to 4 LayerNorms' (partials, dγ, dβ) reduced by one launch (blockIdx.z)
+    const float* part_g[4];
+    const float* part_b[4];
+    float* dgamma[4];
+    float* dbeta[4];
+};
+
+__global__ __launch_bounds__(1024) void ln_param_reduce_kernel(LnReduceJobs jobs, int nparts, int E) {
+    __shared__ float red[16][64];
+    const int z = blockIdx.z;
+    const float* part = blockIdx.y == 0 ? jobs.part_g[z] : jobs.part_b[z];
+    float* out = blockIdx.y == 0 ? jobs.dgamma[z] : jobs.dbeta[z];
     const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (c < E) {
-        int r = rl;
-        for (; r + 12 < nparts; r += 16) {
-            s0 += part[(size_t)r * E + c];
-            s1 += part[(size_t)(r + 4) * E + c];
-            s2 += part[(size_t)(r + 8) * E + c];
-            s3 += part[(size_t)(r + 12) * E + c];
+    float acc = 0.f;
+    for (int base = 0; base < nparts; base += 256) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int r = base + rl + 16 * j;
+            v[j] = c < E && r < nparts ? part[(size_t)r * E + c] : 0.f;
         }
-        for (; r < nparts; r += 4) s0 += part[(size_t)r * E + c];
+#pragma unroll
+        for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+            for (int j = 0; j < 16; j += 2 * w) v[j] += v[j + w];
+        acc += v[0];
     }
-    red[rl][cl] = (s0 + s1) + (s2 + s3);
+    red[rl][cl] = acc;
     __syncthreads();
-    if (rl == 0 && c < E) out[c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    if (rl == 0 && c < E) {
+        float t[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t[j] = red[j][cl];
+#pragma unroll
+        for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+            for (int j = 0; j < 16; j += 2 * w) t[j] += t[j + w];
+        out[c] = t[0];
+    }
 }
 
 // ---- column sums: out[c] (+)= Σ_r X[r][c] -------------------------------------------------
@@ -328,20 +355,29 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
     }
     return check_launch("layernorm_bwd");
 }
 
+int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
+                             float* const* dgamma, float* const* dbeta, hipStream_t s) {
+    ERGM_CHECK_ARG(n >= 1 && n <= 4, "layernorm_param_reduce: 1..4 jobs per launch");
+    LnReduceJobs j{};
+    for (int i = 0; i < n; ++i) {
+        ERGM_CHECK_ARG(part_g[i] && part_b[i] && dgamma[i] && dbeta[i], "layernorm_param_reduce: null argument");
+        j.part_g[i] = part_g[i]; j.part_b[i] = part_b[i]; j.dgamma[i] = dgamma[i]; j.dbeta[i] = dbeta[i];
+    }
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2, n), dim3(1024), 0, s, j, ln_bwd_nparts(rows), E);
+    return check_launch("layernorm_param_reduce");
+}
+
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s) {
-    ERGM_CHECK_ARG(part_g && part_b && dgamma && dbeta, "layernorm_param_reduce: null argument");
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2), dim3(256), 0, s, part_g, part_b,
-                       ln_bwd_nparts(rows), E, dgamma, dbeta);
-    return check_launch("layernorm_param_reduce");
+    return layernorm_param_reduce_n(1, &part_g, &part_b, rows, E, &dgamma, &dbeta, s);
 }
 }  // namespace ergm
 

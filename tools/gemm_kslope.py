@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ergm_amd import _lib as L  # noqa: E402
 
 CFGS = {0: (64, 64), 2: (128, 128), 6: (256, 256), 7: (128, 64), 10: (128, 128), 11: (64, 64), 12: (128, 64),
-        13: (64, 128), 14: (128, 128), 15: (128, 128), 16: (256, 128)}
+        13: (64, 128), 14: (128, 128), 15: (128, 128)}
 
 
 def main():

@@ -55,7 +55,7 @@ if "--phases" in sys.argv:
             cur = "loss+head bwd"
         elif 'attn_bwd' in n and cur == "loss+head bwd":
             cur = "layers bwd"
-        elif 'embed_sort' in n:
+        elif 'embed_runsum' in n:
             cur = "embed bwd"
         q = r['Queue_Id'] + '/' + r['Stream_Id']
         cls = ('gemm' if 'gemm' in n or 'splitk' in n else 'attn' if 'attn' in n else
