@@ -1,8 +1,8 @@
 // Cross-entropy losses of GPT2LMHeadModel for gfx950.
 //
 // LM loss: CrossEntropyLoss(ignore_index=-100, mean) on logits[..., :-1, :] vs labels[..., 1:]
-// (src/model.py:704-708) — one workgroup per logits row keeps the whole bf16 row in registers
-// (single HBM read), computes max / Σexp / LSE with wave shuffles, and writes
+// (src/model.py:704-708) — one 512-thread workgroup per logits row keeps the whole bf16 row in
+// registers (single HBM read), computes max / Σexp / LSE with one fused block reduction, and writes
 // dlogits = (softmax − onehot)/n_valid in the same pass (forward and backward fused; the shift is
 // pure indexing: row (b, s) is scored against labels[b][s+1]).
 // Emotion loss: emotion_head on the last token + CrossEntropyLoss (src/model.py:700-701,710-711).
@@ -10,26 +10,25 @@
 
 namespace ergm {
 
-constexpr int XE_THREADS = 256;
-constexpr int XE_MAXCH = 32;  // 16-B chunks per thread: rows up to 32*256*8 = 65536 columns
+constexpr int XE_THREADS = 512;  // one workgroup per logits row; 8 waves
+constexpr int XE_MAXCH = 16;     // 16-B chunks per thread: rows up to 16*512*8 = 65536 columns
 
-__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    v = is_max ? wave_max(v) : wave_sum(v);
-    __syncthreads();
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    float r = red[0];
-#pragma unroll
-    for (int w = 1; w < XE_THREADS / 64; ++w) r = is_max ? fmaxf(r, red[w]) : r + red[w];
-    return r;
+// (max, Σexp) pair of online softmax: combine two partial pairs
+__device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s2) {
+    const float mn = fmaxf(m, m2);
+    if (mn == -INFINITY) return;
+    s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+    m = mn;
 }
 
+// Row in registers (NCH chunks of 8 bf16 per thread: a single HBM read), one fused block reduction
+// of the per-thread (max, Σexp) pairs, LSE, and dlogits = (softmax − onehot)/n_valid in the same pass.
+template <int NCH>
 __global__ __launch_bounds__(XE_THREADS) void xent_kernel(const __bf16* __restrict__ logits, int ldl,
                                                           const int64_t* __restrict__ labels,
                                                           const int* __restrict__ n_valid, float* __restrict__ row_loss,
-                                                          __bf16* __restrict__ dlogits, int S, int V, int nch) {
-    __shared__ float red[XE_THREADS / 64];
+                                                          __bf16* __restrict__ dlogits, int S, int V) {
+    __shared__ float red_m[XE_THREADS / 64], red_s[XE_THREADS / 64];
     __shared__ float tgt_logit;
     const int t = blockIdx.x;
     const int b = t / S, s = t % S;
@@ -37,18 +36,6 @@ __global__ __launch_bounds__(XE_THREADS) void xent_kernel(const __bf16* __restri
     if (s < S - 1) target = labels[(size_t)b * S + s + 1];
     const bool valid = target >= 0 && target < V;
     const __bf16* row = logits + (size_t)t * ldl;
-    bf16x8 x[XE_MAXCH];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < XE_MAXCH; ++i) {
-        int ch = threadIdx.x + i * XE_THREADS;
-        if (i < nch && ch * 8 < ldl) {
-            x[i] = *reinterpret_cast<const bf16x8*>(row + ch * 8);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (ch * 8 + j < V) mx = fmaxf(mx, bf2f(x[i][j]));
-        }
-    }
     if (!valid) {
         if (threadIdx.x == 0) row_loss[t] = 0.f;
         if (dlogits) {
@@ -60,36 +47,65 @@ __global__ __launch_bounds__(XE_THREADS) void xent_kernel(const __bf16* __restri
         }
         return;
     }
-    mx = block_reduce(mx, red, true);
+    bf16x8 x[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int ch = threadIdx.x + i * XE_THREADS;
+        if (ch * 8 < ldl) x[i] = *reinterpret_cast<const bf16x8*>(row + ch * 8);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int ch = threadIdx.x + i * XE_THREADS;
+        if (ch * 8 < ldl) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (ch * 8 + j < V) mx = fmaxf(mx, bf2f(x[i][j]));
+        }
+    }
     float se = 0.f;
 #pragma unroll
-    for (int i = 0; i < XE_MAXCH; ++i) {
-        int ch = threadIdx.x + i * XE_THREADS;
-        if (i < nch && ch * 8 < ldl) {
+    for (int i = 0; i < NCH; ++i) {
+        const int ch = threadIdx.x + i * XE_THREADS;
+        if (ch * 8 < ldl) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                int c = ch * 8 + j;
+                const int c = ch * 8 + j;
                 if (c < V) se += __expf(bf2f(x[i][j]) - mx);
                 if (c == target) tgt_logit = bf2f(x[i][j]);
             }
         }
     }
-    se = block_reduce(se, red, false);  // its barriers also publish tgt_logit
+    // wave then block combine of (max, Σexp)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(se, o, 64);
+        ms_combine(mx, se, m2, s2);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        red_m[wave] = mx;
+        red_s[wave] = se;
+    }
+    __syncthreads();  // also publishes tgt_logit
+    mx = red_m[0];
+    se = red_s[0];
+#pragma unroll
+    for (int w = 1; w < XE_THREADS / 64; ++w) ms_combine(mx, se, red_m[w], red_s[w]);
     const float lse = mx + logf(se);
     if (threadIdx.x == 0) row_loss[t] = lse - tgt_logit;
     if (!dlogits) return;
     const float inv_n = 1.0f / (float)max(1, *n_valid);
-    const float inv_se = 1.0f / se;
 #pragma unroll
-    for (int i = 0; i < XE_MAXCH; ++i) {
-        int ch = threadIdx.x + i * XE_THREADS;
-        if (i < nch && ch * 8 < ldl) {
+    for (int i = 0; i < NCH; ++i) {
+        const int ch = threadIdx.x + i * XE_THREADS;
+        if (ch * 8 < ldl) {
             bf16x8 d;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                int c = ch * 8 + j;
+                const int c = ch * 8 + j;
                 float g = 0.f;
-                if (c < V) g = (__expf(bf2f(x[i][j]) - mx) * inv_se - (c == target ? 1.f : 0.f)) * inv_n;
+                if (c < V) g = (__expf(bf2f(x[i][j]) - lse) - (c == target ? 1.f : 0.f)) * inv_n;
                 d[j] = f2bf(g);
             }
             *reinterpret_cast<bf16x8*>(dlogits + (size_t)t * ldl + ch * 8) = d;
@@ -221,9 +237,15 @@ extern "C" int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* lab
     int nch = cdiv(cdiv(ldl, 8), XE_THREADS);
     ERGM_CHECK_ARG(nch <= XE_MAXCH, "xent: row of %d columns too long", ldl);
     ERGM_CHECK_ARG(grad_scale == 1.0f, "xent: grad_scale is applied by the consumer GEMMs (pass 1)");
-    hipLaunchKernelGGL(xent_kernel, dim3(B * S), dim3(XE_THREADS), 0, as_stream(stream),
-                       reinterpret_cast<const __bf16*>(logits), ldl, labels, n_valid_global, row_loss,
-                       reinterpret_cast<__bf16*>(dlogits), S, V, nch);
+    const auto* lg = reinterpret_cast<const __bf16*>(logits);
+    auto* dl = reinterpret_cast<__bf16*>(dlogits);
+    hipStream_t s = as_stream(stream);
+    dim3 grid(B * S), blk(XE_THREADS);
+    if (nch <= 2) hipLaunchKernelGGL(xent_kernel<2>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 4) hipLaunchKernelGGL(xent_kernel<4>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 8) hipLaunchKernelGGL(xent_kernel<8>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 13) hipLaunchKernelGGL(xent_kernel<13>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else hipLaunchKernelGGL(xent_kernel<16>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
     return check_launch("xent");
 }
 
