@@ -193,12 +193,13 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
 // global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
 // (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
 // the staging buffer is (BM/WGM)*(BN+4) floats.  slab != nullptr: raw f32 split-K partials.
-template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN>
+template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
                                            float alpha, float* slab) {
+    // NT: every thread of the workgroup (a warp-specialised kernel adds producer waves, which only
+    // help with the copy-out; accumulator fragments come from the WGM x WGN consumer waves)
     constexpr int LD = BN + 4;  // lanes l and l+16 (rows 4 apart) land 16 banks apart
     constexpr int WM = BM / WGM, WN = BN / WGN;
-    constexpr int NT = 64 * WGM * WGN;
     float* t = reinterpret_cast<float*>(lds);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave / WGN, wn = wave % WGN;
@@ -206,7 +207,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
 #pragma unroll
     for (int pass = 0; pass < WGM; ++pass) {
         __syncthreads();
-        if (wm == pass) {
+        if (wave < WGM * WGN && wm == pass) {
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -478,6 +479,87 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
 }
 
+// Warp-specialised variant: NP producer waves only issue the LDS-DMA fills, the WGM x WGN consumer
+// waves only read fragments and run MFMAs.  In gemm_pipe_kernel every wave issues its share of the
+// DMAs and then computes, so the DMA issue time (the per-CU fill path sustains ~100-120 GB/s, about
+// 150 ns per 16 KiB stage: tools/fill_bench.hip) adds to the compute time of every K step; split
+// across waves it overlaps instead, and a K step costs max(fill, compute).  One s_barrier per K step:
+// producers arrive once their DMAs of stage kt have landed, consumers once they are done reading
+// the slot the next fill overwrites.
+template <int BM, int BN, int WGM, int WGN, int NP, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(64 * (WGM * WGN + NP)) void gemm_ws_kernel(GemmArgs a) {
+    constexpr int NC = WGM * WGN;
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
+    constexpr int STAGE = A_BYTES + B_BYTES;
+    constexpr int LPS = GldsTile<BM, A_KM, NP>::PER_WAVE + GldsTile<BN, B_KN, NP>::PER_WAVE;  // per producer
+    static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int id = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = blockIdx.z * a.k_per_split;
+    const int kend = min(a.K, kbeg + a.k_per_split);
+    const int nk = (kend - kbeg) / GEMM_BK;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool producer = wave >= NC;
+    const int pw = wave - NC;
+    const int wm = wave / WGN, wn = wave % WGN;
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_stage = [&](int kt) {
+        char* st = smem + (kt % NS) * STAGE;
+        const int k0 = kbeg + kt * GEMM_BK;
+        GldsTile<BM, A_KM, NP>::issue(st, a.A, a.lda, m0, a.M, k0, pw);
+        GldsTile<BN, B_KN, NP>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, pw);
+    };
+    if (producer) {
+#pragma unroll
+        for (int s = 0; s < NS - 1; ++s)
+            if (s < nk) issue_stage(s);
+    }
+    FragReader<BM, A_KM> la;
+    FragReader<BN, B_KN> lb;
+    for (int kt = 0; kt < nk; ++kt) {
+        if (producer) wait_stages<LPS, NS - 2>(min(NS - 2, nk - 1 - kt));  // stage kt landed
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         // reads of slot kt-1 done
+        __builtin_amdgcn_s_barrier();
+        if (producer) {
+            if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+        } else {
+            const char* st = smem + (kt % NS) * STAGE;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fa[FM], fb[FN];
+#pragma unroll
+                for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
+    // store_tile opens with a barrier: the last stage's reads are done before the staging reuse
+    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * (NC + NP)>(a, smem, acc, m0, n0, alpha, slab);
+}
+
 // split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
 template <int EPI, bool OUT_BF16>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int splits) {
@@ -498,6 +580,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int spli
 // Pipelined-kernel configurations (tile BM x BN, wave grid WGM x WGN, LDS stages NS).
 struct PipeCfg {
     int bm, bn, wgm, wgn, ns;
+    int np = 0;  // > 0: warp-specialised kernel with np producer waves
 };
 static constexpr PipeCfg kCfgs[] = {
     {64, 64, 2, 2, 4},     // 0
@@ -516,6 +599,15 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 6},    // 13
     {128, 128, 2, 2, 4},   // 14
     {128, 128, 4, 2, 4},   // 15 8 waves
+    // warp-specialised (consumer grid + 4 producer waves)
+    {64, 64, 2, 2, 4, 4},    // 16
+    {64, 64, 2, 2, 6, 4},    // 17
+    {128, 64, 2, 2, 5, 4},   // 18
+    {64, 128, 2, 2, 5, 4},   // 19
+    {128, 128, 2, 2, 4, 4},  // 20
+    {128, 128, 4, 2, 4, 4},  // 21
+    {256, 128, 4, 2, 3, 4},  // 22
+    {256, 256, 4, 2, 2, 4},  // 23
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -530,6 +622,15 @@ struct GemmPlan {
 
 static long tiles_of(int M, int N, int bm, int bn) { return (long)cdiv(M, bm) * cdiv(N, bn); }
 
+// Layout / epilogue / output-type combinations instantiated for the pipelined kernels (the ones the
+// training step issues); everything else runs on the register-staged kernel.
+static constexpr bool combo_ok(bool akm, bool bkn, int e, bool ob) {
+    return (!akm && bkn && (e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) && ob) ||
+           (!akm && bkn && e == ERGM_EPI_BIAS_RESID && !ob) || (!akm && bkn && e == ERGM_EPI_NONE && !ob) ||
+           (!akm && !bkn && e == ERGM_EPI_NONE) || (!akm && !bkn && e == ERGM_EPI_GELU_BWD && ob) ||
+           (akm && bkn && e == ERGM_EPI_NONE && !ob);
+}
+
 static bool pipe_ok(const ergm_gemm_desc* d) {
     // the pipelined path needs K % 64 == 0 and 16-B vector epilogue access (N, ldc, aux lds % 8)
     return d->K % GEMM_BK == 0 && d->N % 8 == 0 && d->ldc % 8 == 0 && (!d->aux || d->ld_aux % 8 == 0) &&
@@ -540,7 +641,7 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
     GemmPlan p;
     const int M = d->M, N = d->N, K = d->K;
     int split = 1;
-    if (!pipe_ok(d)) {
+    if (!pipe_ok(d) || !combo_ok(d->a_layout == ERGM_KM, d->b_layout == ERGM_KN, d->epilogue, d->c_dtype == ERGM_BF16)) {
         p.cfg = -1;
         const long t128 = tiles_of(M, N, 128, 128), t64 = tiles_of(M, N, 64, 64);
         p.bm = p.bn = t128 >= 240 ? 128 : 64;
@@ -582,19 +683,24 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
 template <int C, bool AKM, bool BKN, int EPI, bool OB>
 static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
+    constexpr int nthreads = 64 * (c.wgm * c.wgn + c.np);
     constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2,
                                     (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
-    auto k = split > 1 ? gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>
-                       : gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>;
-    static bool attr = (hipFuncSetAttribute((const void*)gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN,
-                                                                          ERGM_EPI_NONE, false>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                        hipFuncSetAttribute((const void*)gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+    using KSplit = decltype(&gemm_pipe_kernel<16, 16, 1, 1, 2, AKM, BKN, ERGM_EPI_NONE, false>);
+    KSplit k_split, k_full;
+    if constexpr (c.np > 0) {
+        k_split = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
+        k_full = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, EPI, OB>;
+    } else {
+        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
+        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>;
+    }
+    static bool attr = (hipFuncSetAttribute((const void*)k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        hipFuncSetAttribute((const void*)k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         true);
     (void)attr;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
-    hipLaunchKernelGGL(k, grid, dim3(64 * c.wgm * c.wgn), lds, s, a);
+    hipLaunchKernelGGL(split > 1 ? k_split : k_full, grid, dim3(nthreads), lds, s, a);
 }
 
 template <bool AKM, bool BKN, int EPI, bool OB>
@@ -615,7 +721,15 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 12: launch_pipe_cfg<12, AKM, BKN, EPI, OB>(a, split, s); break;
         case 13: launch_pipe_cfg<13, AKM, BKN, EPI, OB>(a, split, s); break;
         case 14: launch_pipe_cfg<14, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<15, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 15: launch_pipe_cfg<15, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 16: launch_pipe_cfg<16, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 17: launch_pipe_cfg<17, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 18: launch_pipe_cfg<18, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 19: launch_pipe_cfg<19, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 20: launch_pipe_cfg<20, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 21: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 22: launch_pipe_cfg<22, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<23, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 
@@ -645,10 +759,7 @@ static void launch_reg_any(const GemmArgs& a, const GemmPlan& p, hipStream_t s) 
 // Layout/epilogue pairs the training step issues get the pipelined kernel family.
 template <bool AKM, bool BKN, int EPI, bool OB>
 static constexpr bool pipe_combo() {
-    return (!AKM && BKN && (EPI == ERGM_EPI_BIAS || EPI == ERGM_EPI_BIAS_GELU) && OB) ||
-           (!AKM && BKN && EPI == ERGM_EPI_BIAS_RESID && !OB) || (!AKM && BKN && EPI == ERGM_EPI_NONE && !OB) ||
-           (!AKM && !BKN && EPI == ERGM_EPI_NONE) || (!AKM && !BKN && EPI == ERGM_EPI_GELU_BWD && OB) ||
-           (AKM && BKN && EPI == ERGM_EPI_NONE && !OB);
+    return combo_ok(AKM, BKN, EPI, OB);
 }
 
 template <bool AKM, bool BKN, int EPI, bool OB>

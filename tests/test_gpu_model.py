@@ -215,3 +215,21 @@ def test_inference_and_argument_errors(gpu):
         model(input_ids=kw["input_ids"])  # caption_ids required (src/model.py:521)
     with pytest.raises(NotImplementedError):
         model(input_ids=kw["input_ids"], caption_ids=kw["caption_ids"], attention_mask=torch.ones(2, 32))
+
+
+def test_iemocap_shape_long_sequence_matches_oracle(gpu):
+    """C4's sequence shape (S=512, 20 turns: attention through the tiled kernels, 3·B·S lookups in
+    the embedding sort) on a small model, against the live oracle."""
+    from ergm_amd.data import synthetic_batch
+    V, E, Lyr, H = 500, 128, 2, 2
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=512)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=512)
+    P0 = O.init_params(ocfg, seed=7)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    batch = synthetic_batch(2, 512, n_turns=20, feat_dim=E, seed=3, vocab_hi=490, sp1=498, sp2=499, eos=489)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    _grad_gate(_grads(model), og)

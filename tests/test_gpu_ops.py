@@ -45,6 +45,37 @@ def test_gemm_layouts(gpu, M, N, K, al, bl):
     assert _rel(outb.float().cpu(), ref) < 6e-3
 
 
+N_CFGS = 24  # kCfgs in gemm.hip (ergm_gemm_tune rejects an index past the table)
+
+
+@pytest.mark.parametrize("cfg", range(N_CFGS))
+def test_gemm_every_pipelined_config(gpu, cfg):
+    """Each pipelined / warp-specialised tile configuration, forced through ergm_gemm_tune, on ragged
+    M/N edges, all four operand layouts, with and without split-K."""
+    lib = L.load()
+    M, N, K = 328, 392, 512
+    g = torch.Generator(device="cpu").manual_seed(cfg)
+    Am, Bm = torch.randn(M, K, generator=g), torch.randn(K, N, generator=g)
+    ref = _bf(Am).double() @ _bf(Bm).double()
+    try:
+        for split in (1, 2):
+            L.check(lib.ergm_gemm_tune(cfg, split), "tune")
+            for al, bl in ((L.MK, L.NK), (L.MK, L.KN), (L.KM, L.NK), (L.KM, L.KN)):
+                A = _bf(Am if al == L.MK else Am.t().contiguous()).to(gpu)
+                B = _bf(Bm.t().contiguous() if bl == L.NK else Bm).to(gpu)
+                out = ops.gemm(A, B, M, N, K, al, bl, out_dtype=torch.float32, split_k=split)
+                assert _rel(out.cpu(), ref) < 1e-5, (split, al, bl)
+        L.check(lib.ergm_gemm_tune(cfg, 1), "tune")
+        W = _bf(Bm).to(gpu)
+        bias = torch.randn(N, device=gpu)
+        out = ops.gemm(_bf(Am).to(gpu), W, M, N, K, L.MK, L.KN, epilogue=L.EPI_BIAS, bias=bias)
+        assert _rel(out.cpu(), ref + bias.double().cpu()) < 1e-5
+    finally:
+        L.check(lib.ergm_gemm_tune(-1, 0), "tune")
+    with pytest.raises(ValueError):
+        L.check(lib.ergm_gemm_tune(N_CFGS, 1), "tune")
+
+
 @pytest.mark.parametrize("split", [2, 3, 5])
 def test_gemm_split_k(gpu, split):
     M, N, K = 192, 320, 2048

@@ -10,8 +10,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ergm_amd import _lib as L  # noqa: E402
 
-CFGS = {0: (64, 64), 2: (128, 128), 6: (256, 256), 7: (128, 64), 10: (128, 128), 11: (64, 64), 12: (128, 64),
-        13: (64, 128), 14: (128, 128), 15: (128, 128)}
+CFGS = {0: (64, 64), 2: (128, 128), 6: (256, 256), 10: (128, 128), 16: (64, 64), 17: (64, 64), 18: (128, 64),
+        19: (64, 128), 20: (128, 128), 21: (128, 128), 22: (256, 128), 23: (256, 256)}
 
 
 def main():

@@ -42,7 +42,8 @@ SHAPES = [
     ("bwd dcap", 1, T, E, L2E, MK, L2E, NK, L2E, L.EPI_NONE, FP),
 ]
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
-        (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128)]
+        (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
+        (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128), (256, 128), (256, 256)]
 REPS = 20
 
 
