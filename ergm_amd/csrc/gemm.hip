@@ -606,8 +606,6 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 5, 4},   // 19
     {128, 128, 2, 2, 4, 4},  // 20
     {128, 128, 4, 2, 4, 4},  // 21
-    {256, 128, 4, 2, 3, 4},  // 22
-    {256, 256, 4, 2, 2, 4},  // 23
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -727,9 +725,7 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 18: launch_pipe_cfg<18, AKM, BKN, EPI, OB>(a, split, s); break;
         case 19: launch_pipe_cfg<19, AKM, BKN, EPI, OB>(a, split, s); break;
         case 20: launch_pipe_cfg<20, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 21: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 22: launch_pipe_cfg<22, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<23, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 

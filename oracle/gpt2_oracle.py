@@ -170,7 +170,9 @@ def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type
     wte, wpe = P["transformer.wte.weight"], P["transformer.wpe.weight"]
     B, S = input_ids.shape
     inputs_embeds = F.embedding(input_ids, wte)                               # :459
-    caption_embeds = F.embedding(caption_ids.view(-1, S), wte)                # :460-463
+    # :460-463 views captions as [-1, S] (caption length == S); [B, -1] is the same for Sc == S and
+    # lets the KV-cache generation test score a response against fixed prompt captions (Sc != S)
+    caption_embeds = F.embedding(caption_ids.view(B, -1), wte)
     enc_mask = torch.zeros(B, 1, 1, caption_embeds.shape[1])                  # :484-489 invert(ones)
     if visual_feat is not None:                                               # :495-498
         vis = visual_feat if visual_feat.dim() == 2 else visual_feat[:, 0]

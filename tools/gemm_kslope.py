@@ -11,15 +11,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ergm_amd import _lib as L  # noqa: E402
 
 CFGS = {0: (64, 64), 2: (128, 128), 6: (256, 256), 10: (128, 128), 16: (64, 64), 17: (64, 64), 18: (128, 64),
-        19: (64, 128), 20: (128, 128), 21: (128, 128), 22: (256, 128), 23: (256, 256)}
+        19: (64, 128), 20: (128, 128), 21: (128, 128)}
 
 
 def main():
     dev = torch.device("cuda:0")
     lib = L.load()
+    per_cu = int(sys.argv[1]) if len(sys.argv) > 1 else 1   # tiles per CU (256 CUs)
     for cfg, (bm, bn) in CFGS.items():
         for al, bl, tag in ((L.MK, L.NK, "MKxNK"), (L.KM, L.KN, "KMxKN")):
-            M, N = bm * 16, bn * 16
+            M, N = bm * 16 * per_cu, bn * 16
             pts = []
             for K in (512, 1024, 2048, 4096):
                 A = torch.randn(M * K, device=dev).bfloat16()
@@ -47,8 +48,8 @@ def main():
             (k0, t0), (k1, t1) = pts[1], pts[-1]
             slope = (t1 - t0) / ((k1 - k0) / 64)  # us per K step
             cyc = slope * 1e-6 * 2.4e9
-            mfma_cyc = bm * bn * 64 * 2 / (2.5e15 / 256 / 2.4e9)  # ideal cycles at per-CU peak
-            fill = (bm + bn) * 64 * 2 / (slope * 1e-6) / 1e9
+            mfma_cyc = per_cu * bm * bn * 64 * 2 / (2.5e15 / 256 / 2.4e9)  # ideal cycles at per-CU peak
+            fill = per_cu * (bm + bn) * 64 * 2 / (slope * 1e-6) / 1e9
             print(f"cfg{cfg:<2d} {bm}x{bn} {tag}: " + " ".join(f"K={k}:{t:.1f}us" for k, t in pts) +
                   f" | step {slope * 1e3:.0f} ns = {cyc:.0f} cyc (MFMA ideal {mfma_cyc:.0f}), fill {fill:.0f} GB/s/CU",
                   flush=True)

@@ -43,7 +43,7 @@ SHAPES = [
 ]
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
         (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
-        (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128), (256, 128), (256, 256)]
+        (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128)]
 REPS = 20
 
 
