@@ -29,14 +29,14 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-def pmc_traffic(probe: int):
+def pmc_traffic(probe: int, config: str = "c2"):
     """HBM bytes per launch of the probed kernel from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from separate rocprofv3
     FETCH_SIZE / WRITE_SIZE passes).  None when no summary covers the probe."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "r*_pmc_traffic.json")))
-    if probe != 1 or not files:
+    if probe != 1 or config != "c2" or not files:  # the committed PMC passes are of the C2 workload
         return None, None
     with open(files[-1]) as f:
         rec = json.load(f).get("lm_head_fwd")
@@ -44,10 +44,13 @@ def pmc_traffic(probe: int):
         return None, None
     return round(rec["hbm_bytes"]), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {
-    # name: (S, turns, batch per GPU, description)
-    "c2": (128, 5, 16, "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
-    "c4": (512, 20, 8, "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
+    # name: (model, S, turns, batch per GPU, pooled feature width, description)
+    "c2": ("small", 128, 5, 16, 768, "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
+    "c4": ("small", 512, 20, 8, 768, "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
+    "c5": ("medium", 128, 5, 32, 768, "GPT-2-medium + 768-d audio/visual features through projection GEMMs, "
+           "MELD-shape (S=128, 5 turns), B=32/GPU"),
 }
+MODELS = {"small": dict(n_embd=768, n_layer=12, n_head=12), "medium": dict(n_embd=1024, n_layer=24, n_head=16)}
 
 
 def flops_per_utterance(S: int, E: int = 768, L: int = 12, V: int = 50260) -> float:
@@ -58,16 +61,16 @@ def flops_per_utterance(S: int, E: int = 768, L: int = 12, V: int = 50260) -> fl
     return 3.0 * S * f_tok
 
 
-def cpu_baseline(S, turns, B, seconds_target=20.0):
+def cpu_baseline(S, turns, B, model="small", feat_dim=768, seconds_target=20.0):
     """Time the CPU oracle (fp32) doing the same train step on a bounded sample."""
     from oracle import gpt2_oracle as O
     from ergm_amd.data import synthetic_batch
     n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     torch.set_num_threads(n)
-    cfg = O.OracleConfig()
+    cfg = O.OracleConfig(**MODELS[model], feat_dim=feat_dim)
     P = O.init_params(cfg, seed=0, perturb=False)
     st = O.AdamWState()
-    batch = synthetic_batch(B, S, n_turns=turns, seed=123)
+    batch = synthetic_batch(B, S, n_turns=turns, seed=123, feat_dim=feat_dim)
     lr = 2e-5
     _, g = O.loss_and_grads(P, cfg, batch)  # warm-up step
     O.adamw_step(P, g, st, lr)
@@ -81,7 +84,7 @@ def cpu_baseline(S, turns, B, seconds_target=20.0):
             break
     return {"value": round(B * steps / el, 4), "unit": "utterances/s", "cores": n, "kind": "port",
             "sample": f"{steps} full fp32 train steps (fwd+bwd+AdamW) of the CPU oracle at B={B}, S={S}, "
-                      f"GPT-2-small+fusion, after 1 warm-up step; torch CPU threads={n}"}
+                      f"GPT-2-{model}+fusion, after 1 warm-up step; torch CPU threads={n}"}
 
 
 def main():
@@ -113,13 +116,13 @@ def main():
         pg = dist.group.WORLD
 
     from ergm_amd import _lib
-    from ergm_amd.config import gpt2_small
+    from ergm_amd.config import ERGMConfig
     from ergm_amd.data import synthetic_batch
     from ergm_amd.model import GPT2LMHeadModel
     from ergm_amd.optim import FusedAdamW, get_polynomial_decay_schedule_with_warmup
 
-    S, turns, B, desc = CONFIGS[args.config]
-    cfg = gpt2_small()
+    mname, S, turns, B, Fd, desc = CONFIGS[args.config]
+    cfg = ERGMConfig(**MODELS[mname], feat_dim=Fd)
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
@@ -128,7 +131,7 @@ def main():
     total = args.warmup + args.steps
     sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=int(0.1 * total),
                                                       num_training_steps=total, power=2)
-    batch = synthetic_batch(B, S, n_turns=turns, seed=1000 + rank)
+    batch = synthetic_batch(B, S, n_turns=turns, seed=1000 + rank, feat_dim=Fd)
     kw = dict(input_ids=batch["input_ids"], token_type_ids=batch["token_type_ids"], labels=batch["labels"],
               emotion_labels=batch["emotion_labels"], caption_ids=batch["caption_ids"], imgs=batch["visual_feat"],
               auds=batch["audio_feat"])
@@ -189,8 +192,9 @@ def main():
     probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
                   2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
     achieved = probe_flops / (probe_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(args.probe)
-    step_flops = flops_per_utterance(S) * B
+    traffic, traffic_src = pmc_traffic(args.probe, args.config)
+    Lyr = cfg.n_layer
+    step_flops = flops_per_utterance(S, E, Lyr, V) * B
     rec = {
         "metric": "utterances/sec training, MELD-shape synthetic batch, 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -203,9 +207,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (seeded MELD-shape token/feature batches; random-init GPT-2-small weights)",
-        "config": {"workload": desc, "model": "GPT-2-small (L=12, E=768, H=12, V=50260) + cross-attention "
-                   "caption fusion + emotion head", "global_batch": B * world, "seq_len": S,
+        "data": f"synthetic (seeded MELD-shape token/feature batches; random-init GPT-2-{mname} weights)",
+        "config": {"workload": desc, "model": f"GPT-2-{mname} (L={Lyr}, E={E}, H={cfg.n_head}, V={V}) + "
+                   "cross-attention caption fusion + emotion head", "global_batch": B * world, "seq_len": S,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": round(achieved, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
@@ -214,7 +218,8 @@ def main():
                      "flops_per_launch": probe_flops},
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                      "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S), 0)},
+                      "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S, E, Lyr, V),
+                                                         0)},
         "optimizer": "FusedAdamW " + (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks})"
                                       if not args.no_overlap_optim else "after backward"),
         "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
@@ -222,7 +227,7 @@ def main():
                           "emotion_acc": round(correct.item() / (B * total), 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(S, turns, B)
+        rec["cpu_baseline"] = cpu_baseline(S, turns, B, mname, Fd)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -36,7 +36,8 @@ class GemmDesc(C.Structure):
 class ModelDims(C.Structure):
     _fields_ = [("vocab", C.c_int), ("vocab_pad", C.c_int), ("n_embd", C.c_int), ("n_layer", C.c_int),
                 ("n_head", C.c_int), ("n_inner", C.c_int), ("n_positions", C.c_int), ("batch", C.c_int),
-                ("seq", C.c_int), ("eps", C.c_float), ("has_features", C.c_int), ("ld_vis", C.c_int)]
+                ("seq", C.c_int), ("eps", C.c_float), ("has_features", C.c_int), ("ld_vis", C.c_int),
+                ("feat_dim", C.c_int)]
 
 
 class ModelParams(C.Structure):
@@ -46,7 +47,10 @@ class ModelParams(C.Structure):
                 ("layer_off", C.c_int64 * 18),
                 ("g_wte", C.c_void_p), ("g_wpe", C.c_void_p), ("g_ln_f_w", C.c_void_p), ("g_ln_f_b", C.c_void_p),
                 ("g_emo_w", C.c_void_p), ("g_capkv_w", C.c_void_p), ("g_capkv_b", C.c_void_p),
-                ("g_layer", C.c_void_p)]
+                ("g_layer", C.c_void_p),
+                ("vproj_w_b", C.c_void_p), ("vproj_b", C.c_void_p), ("aproj_w_b", C.c_void_p),
+                ("aproj_b", C.c_void_p), ("g_vproj_w", C.c_void_p), ("g_vproj_b", C.c_void_p),
+                ("g_aproj_w", C.c_void_p), ("g_aproj_b", C.c_void_p)]
 
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t

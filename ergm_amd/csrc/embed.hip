@@ -377,3 +377,49 @@ extern "C" int ergm_rows_compact(const void* row_flag, const int* pos, int n, in
                        (const uint8_t*)row_flag, pos, n, row_len / 4, (float4*)compact, (float4*)dst, mode);
     return check_launch("rows_compact");
 }
+
+// ---- feature projection operands (build-side config 5: feat_dim != n_embd) --------
+namespace ergm {
+
+// out[m][b][k] (bf16, [2][Bp][ld]) = bf16(src_m[b][k]) for b < B, 0 for the pad rows b in [B, Bp);
+// src_0 = the visual row 0 (vis + b*ld_vis), src_1 = the audio vector (aud + b*Fd).  Column Fd is the
+// constant 1 of the fused-bias weight-gradient GEMM, columns Fd+1 .. ld-1 are 0.
+__global__ __launch_bounds__(256) void feat_pack_kernel(const float* __restrict__ vis, int ld_vis,
+                                                        const float* __restrict__ aud, __bf16* __restrict__ out,
+                                                        int B, int Bp, int Fd, int ld) {
+    const int row = blockIdx.x;  // m * Bp + b
+    const int m = row / Bp, b = row % Bp;
+    const float* src = b < B ? (m == 0 ? vis + (size_t)b * ld_vis : aud + (size_t)b * Fd) : nullptr;
+    __bf16* dst = out + (size_t)row * ld;
+    for (int k = threadIdx.x; k < ld; k += 256) {
+        float v = k < Fd ? (src ? src[k] : 0.f) : (k == Fd ? 1.f : 0.f);
+        dst[k] = f2bf(v);
+    }
+}
+
+// d[m][b][n] (bf16, [2][Bp][E]) = bf16(dh0[b*S + m][n]) for b < B (the gradient reaching the
+// projected visual (m=0, position 0) and audio (m=1, position 1) vectors), 0 for the pad rows.
+__global__ __launch_bounds__(256) void proj_grad_pack_kernel(const float* __restrict__ dh0, __bf16* __restrict__ d,
+                                                             int B, int Bp, int S, int E) {
+    const int row = blockIdx.x;
+    const int m = row / Bp, b = row % Bp;
+    for (int n = threadIdx.x; n < E; n += 256)
+        d[(size_t)row * E + n] = f2bf(b < B ? dh0[((size_t)b * S + m) * E + n] : 0.f);
+}
+
+int feat_pack(const float* vis, int ld_vis, const float* aud, void* out, int B, int Bp, int Fd, int ld,
+              hipStream_t s) {
+    ERGM_CHECK_ARG(vis && aud && out && B > 0 && Bp >= B && ld > Fd, "feat_pack: bad argument");
+    hipLaunchKernelGGL(feat_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, vis, ld_vis, aud,
+                       reinterpret_cast<__bf16*>(out), B, Bp, Fd, ld);
+    return check_launch("feat_pack");
+}
+
+int proj_grad_pack(const float* dh0, void* d, int B, int Bp, int S, int E, hipStream_t s) {
+    ERGM_CHECK_ARG(dh0 && d && B > 0 && Bp >= B && S >= 2, "proj_grad_pack: bad argument");
+    hipLaunchKernelGGL(proj_grad_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, dh0, reinterpret_cast<__bf16*>(d), B, Bp,
+                       S, E);
+    return check_launch("proj_grad_pack");
+}
+
+}  // namespace ergm

@@ -40,6 +40,8 @@ int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
                    uint8_t* row_flag, int n_flag, hipStream_t s);
 int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
                    float* dwpe, float* part, const int* row_pos, hipStream_t s);
+int feat_pack(const float* vis, int ld_vis, const float* aud, void* out, int B, int Bp, int Fd, int ld, hipStream_t s);
+int proj_grad_pack(const float* dh0, void* d, int B, int Bp, int S, int E, hipStream_t s);
 }  // namespace ergm
 
 struct LayerActs {
@@ -66,6 +68,15 @@ struct ergm_model_plan {
     __bf16* dlogits;
     float *row_loss, *emo_sum, *emo_tmp;
     int* n_valid_local;
+    // feature projections (feat_dim != n_embd): bf16 operands [2][Bp][Fd+8] (visual rows, then audio
+    // rows; ones column at Fd for the fused bias gradient; batch padded to Bp = round64(B) zero rows so
+    // the weight-gradient GEMM's contraction over the batch is a whole K tile), projected vectors f32
+    // [2][Bp][E] (what the embedding kernel injects), their bf16 gradients [2][Bp][E]
+    bool proj;
+    int Fd, Bp;
+    __bf16* feat_b16;
+    float* proj_out;
+    __bf16* dproj;
     // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
@@ -153,6 +164,18 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->emo_sum = c.take<float>(4);
     P->emo_tmp = c.take<float>((size_t)d.batch * 16 + 8);
     P->n_valid_local = c.take<int>(4);
+    P->Fd = d.feat_dim > 0 ? d.feat_dim : (int)E;
+    P->proj = d.has_features && P->Fd != (int)E;
+    P->Bp = (d.batch + 63) / 64 * 64;
+    if (P->proj) {
+        P->feat_b16 = c.take<__bf16>((size_t)2 * P->Bp * (P->Fd + 8));
+        P->proj_out = c.take<float>((size_t)2 * P->Bp * E);
+        P->dproj = c.take<__bf16>((size_t)2 * P->Bp * E);
+    } else {
+        P->feat_b16 = nullptr;
+        P->proj_out = nullptr;
+        P->dproj = nullptr;
+    }
     P->keys = c.take<uint64_t>(3 * T);
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
@@ -326,6 +349,15 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     ERGM_CHECK_ARG(d.batch > 0 && d.seq >= 2 && d.seq <= d.n_positions, "model_create: bad batch/seq");
     ERGM_CHECK_ARG((d.batch * d.seq) % 8 == 0, "model_create: B*S must be a multiple of 8");
     ERGM_CHECK_ARG(d.n_layer > 0, "model_create: n_layer must be > 0");
+    ERGM_CHECK_ARG(d.feat_dim >= 0 && d.feat_dim % 64 == 0, "model_create: feat_dim must be a multiple of 64");
+    if (d.has_features && d.feat_dim > 0 && d.feat_dim != d.n_embd) {
+        const ergm_model_params& q = *params;
+        ERGM_CHECK_ARG(q.vproj_w_b && q.vproj_b && q.aproj_w_b && q.aproj_b && q.g_vproj_w && q.g_aproj_w,
+                       "model_create: feat_dim %d != n_embd needs the projection parameters", d.feat_dim);
+        const int64_t wsz = (int64_t)d.feat_dim * d.n_embd;
+        ERGM_CHECK_ARG(q.g_vproj_b == q.g_vproj_w + wsz && q.g_aproj_b == q.g_aproj_w + wsz,
+                       "model_create: projection bias gradients must follow their weights");
+    }
     size_t need = ergm_model_workspace_size(dims);
     ERGM_CHECK_ARG(ws_bytes >= need, "model_create: workspace %zu < %zu bytes", ws_bytes, need);
     auto* P = new (std::nothrow) ergm_model_plan();
@@ -447,8 +479,24 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     const int L2E = P->L2E;
     const ergm_model_params& p = P->p;
 
+    const float* vis_in = P->vis;
+    const float* aud_in = P->aud;
+    int ld_vis = d.ld_vis;
+    if (P->proj && (P->dry || P->vis)) {
+        // build-side feature projections (config 5): [Bp][Fd]·[Fd][E] + b per modality, MFMA GEMMs
+        const int Fd = P->Fd, Bp = P->Bp, ldf = P->Fd + 8;
+        if (!P->dry) ERGM_TRY(feat_pack(P->vis, d.ld_vis, P->aud, P->feat_b16, B, Bp, Fd, ldf, s));
+        ERGM_TRY(gemm(P, s, Bp, E, Fd, P->feat_b16, ldf, ERGM_MK, p.vproj_w_b, E, ERGM_KN, P->proj_out, E, ERGM_F32,
+                      ERGM_EPI_BIAS, p.vproj_b));
+        ERGM_TRY(gemm(P, s, Bp, E, Fd, P->feat_b16 ? P->feat_b16 + (size_t)Bp * ldf : nullptr, ldf, ERGM_MK,
+                      p.aproj_w_b, E, ERGM_KN, P->proj_out ? P->proj_out + (size_t)Bp * E : nullptr, E, ERGM_F32,
+                      ERGM_EPI_BIAS, p.aproj_b));
+        vis_in = P->proj_out;
+        aud_in = P->proj_out ? P->proj_out + (size_t)Bp * E : nullptr;
+        ld_vis = E;
+    }
     if (!P->dry)
-        ERGM_TRY(embed_fwd_ld(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, P->vis, d.ld_vis, P->aud, P->resid[0], P->cap,
+        ERGM_TRY(embed_fwd_ld(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, vis_in, ld_vis, aud_in, P->resid[0], P->cap,
                               P->XE, B, S, E, d.vocab, s));
     // all L cross-attention K/V projections of the caption embeddings in one GEMM, on the side stream
     // (it overlaps block 0's self-attention; joined before block 0's cross-attention)
@@ -636,6 +684,26 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, L2E = P->L2E, L = d.n_layer;
+    if (P->proj) {
+        // feature projections: the projected vectors got dh0 at positions 0 / 1; dW = featᵀ·d over the
+        // (padded) batch with the bias row fused (side stream); no gradient flows to the features
+        const int Fd = P->Fd, Bp = P->Bp, ldf = P->Fd + 8;
+        if (P->dry || P->vis) {
+            if (!P->dry) ERGM_TRY(proj_grad_pack(P->dh, P->dproj, d.batch, Bp, d.seq, E, s));
+            ERGM_TRY(fork_side(P, s));
+            hipStream_t ss = P->dry ? s : P->side;
+            for (int m = 0; m < 2; ++m) {
+                float* gw = m == 0 ? p.g_vproj_w : p.g_aproj_w;
+                ERGM_TRY(gemm(P, ss, Fd + 1, E, Bp, P->feat_b16 ? P->feat_b16 + (size_t)m * Bp * ldf : nullptr, ldf,
+                              ERGM_KM, P->dproj ? P->dproj + (size_t)m * Bp * E : nullptr, E, ERGM_KN, gw, E, ERGM_F32,
+                              ERGM_EPI_NONE));
+            }
+        } else {  // text-only batch through a projected model: zero projection gradients
+            const size_t n = ((size_t)Fd + 1) * E * sizeof(float);
+            if (hipMemsetAsync(p.g_vproj_w, 0, n, s) != hipSuccess || hipMemsetAsync(p.g_aproj_w, 0, n, s) != hipSuccess)
+                return fail(ERGM_EHIP, "model: memset");
+        }
+    }
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
     ERGM_TRY(dw_gemm(P, s, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
     ERGM_TRY(side_mark(P, L + 2));

@@ -60,7 +60,7 @@ def _as_config(config) -> ERGMConfig:
     return ERGMConfig(vocab_size=g("vocab_size"), n_embd=g("n_embd"), n_layer=g("n_layer"), n_head=g("n_head"),
                       n_positions=g("n_positions", 1024), n_inner=g("n_inner"),
                       layer_norm_epsilon=g("layer_norm_epsilon", 1e-5),
-                      initializer_range=g("initializer_range", 0.02))
+                      initializer_range=g("initializer_range", 0.02), feat_dim=g("feat_dim"))
 
 
 class _FusedTrainStep(torch.autograd.Function):
@@ -118,7 +118,8 @@ class GPT2LMHeadModel(nn.Module):
             raise ValueError(f"head_dim must be 64 for the fused attention kernels (got {cfg.head_dim})")
         self.config = cfg
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.layout = build_layout(cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.inner, cfg.n_positions)
+        self.layout = build_layout(cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.inner, cfg.n_positions,
+                                   feat_dim=cfg.feat_dim)
         n = self.layout.total
         self.flat = nn.Parameter(torch.zeros(n, dtype=torch.float32, device=dev))
         self.register_buffer("flat_b16", torch.zeros(n, dtype=torch.bfloat16, device=dev), persistent=False)
@@ -242,7 +243,7 @@ class GPT2LMHeadModel(nn.Module):
             raise ValueError("imgs/visual_feat and auds/audio_feat must be given together (src/model.py:495-498)")
         dev = self.flat.device
         B, S = input_ids.shape
-        E = self.config.n_embd
+        Fd = self.layout.Fd
 
         def dv(t, dtype):
             return None if t is None else t.to(dev, dtype, non_blocking=True).contiguous()
@@ -259,8 +260,8 @@ class GPT2LMHeadModel(nn.Module):
             aud = dv(aud, torch.float32)
             if vis.dim() == 2:
                 vis = vis.unsqueeze(1)
-            if vis.shape[0] != B or vis.shape[-1] != E or tuple(aud.shape) != (B, E):
-                raise ValueError(f"visual [B,Tv,{E}] / audio [B,{E}] features expected, got {tuple(vis.shape)} / "
+            if vis.shape[0] != B or vis.shape[-1] != Fd or tuple(aud.shape) != (B, Fd):
+                raise ValueError(f"visual [B,Tv,{Fd}] / audio [B,{Fd}] features expected, got {tuple(vis.shape)} / "
                                  f"{tuple(aud.shape)}")
             vis_rows = vis.shape[1]
         if S > self.config.n_positions:

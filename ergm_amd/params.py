@@ -5,12 +5,18 @@ read, and one fp32 gradient buffer with the same layout).  The order is the orde
 backward pass finishes each tensor's gradient, so data-parallel all-reduce buckets are contiguous
 ranges that become ready one after another:
 
-    emotion_head | ln_f | block L-1 | ... | block 0 | stacked caption K/V proj (all blocks) | wpe | wte
+    emotion_head | ln_f | block L-1 | ... | block 0 | stacked caption K/V proj (all blocks) | wpe
+    | [visual_proj | audio_proj] | wte
 
 The tied ``wte``/``lm_head`` weight is padded to a multiple of 64 rows with zero rows (zero logits,
 zero gradients, AdamW keeps them 0) so the LM-head GEMMs need no N/K tail handling.  The
 cross-attention ``c_attn`` weights of all blocks are stored stacked as one [E, L·2E] matrix (the
 caption K/V projections of every block run as one GEMM); per-block names are strided views.
+
+When the pooled audio / visual features are narrower than the backbone (config 5: 768-d features,
+n_embd 1024) the layout also holds the build-side feature projections ``transformer.visual_proj`` /
+``transformer.audio_proj`` (Conv1D [Fd, E] + bias, bias right after its weight); the reference has no
+such tensors (it adds 768-d features to a 768-d stream, src/model.py:497-498).
 
 Names follow the reference state_dict (src/model.py:94-99,257-258,276-284,387-392,605,608).
 """
@@ -50,6 +56,7 @@ class Layout:
     L: int
     F: int
     P: int
+    Fd: int                   # pooled feature width (== E: no projection)
     total: int
     views: Dict[str, View]
     layer_base: List[int]     # element offset of block i's tensor group
@@ -61,7 +68,8 @@ class Layout:
         return [f"transformer.h.{i}." + t for t in LAYER_TENSORS]
 
 
-def build_layout(vocab: int, E: int, L: int, F: int, P: int, num_emotions: int = 7) -> Layout:
+def build_layout(vocab: int, E: int, L: int, F: int, P: int, num_emotions: int = 7, feat_dim=None) -> Layout:
+    Fd = E if not feat_dim else feat_dim
     vocab_pad = _al(vocab)
     views: Dict[str, View] = {}
     seg: Dict[str, Tuple[int, int]] = {}
@@ -107,6 +115,10 @@ def build_layout(vocab: int, E: int, L: int, F: int, P: int, num_emotions: int =
     views["__capkv_w"] = View(capw, (E, L * 2 * E), (L * 2 * E, 1))
     views["__capkv_b"] = View(capb, (L * 2 * E,), (1,))
     put("transformer.wpe.weight", (P, E))
+    if Fd != E:
+        for m in ("visual_proj", "audio_proj"):
+            put(f"transformer.{m}.weight", (Fd, E))
+            put(f"transformer.{m}.bias", (E,))
     seg["capwpe"] = (s0, off)
     wte_off = off
     views["transformer.wte.weight"] = View(wte_off, (vocab, E), (E, 1))
@@ -114,7 +126,7 @@ def build_layout(vocab: int, E: int, L: int, F: int, P: int, num_emotions: int =
     off = _al(off + vocab_pad * E)
     seg["wte"] = (wte_off, off)
     seg["embed"] = (s0, off)
-    return Layout(vocab, vocab_pad, E, L, F, P, off, views, layer_base, layer_stride, layer_off, seg)
+    return Layout(vocab, vocab_pad, E, L, F, P, Fd, off, views, layer_base, layer_stride, layer_off, seg)
 
 
 def state_dict_names(layout: Layout) -> List[str]:
@@ -128,6 +140,8 @@ def state_dict_names(layout: Layout) -> List[str]:
     for i in range(layout.L):
         names += [f"transformer.h.{i}." + t for t in order]
     names += ["transformer.ln_f.weight", "transformer.ln_f.bias", "lm_head.weight", "emotion_head.weight"]
+    if layout.Fd != layout.E:  # build-side feature projections (config 5)
+        names += [f"transformer.{m}.{t}" for m in ("visual_proj", "audio_proj") for t in ("weight", "bias")]
     return names
 
 

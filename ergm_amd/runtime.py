@@ -35,7 +35,7 @@ class ModelRunner:
         self.dims = L.ModelDims(vocab=layout.vocab, vocab_pad=layout.vocab_pad, n_embd=E, n_layer=Lyr,
                                 n_head=cfg.n_head, n_inner=layout.F, n_positions=layout.P, batch=B, seq=S,
                                 eps=cfg.layer_norm_epsilon, has_features=int(has_features),
-                                ld_vis=vis_rows * E if has_features else 0)
+                                ld_vis=vis_rows * layout.Fd if has_features else 0, feat_dim=layout.Fd)
         ws_bytes = self.lib.ergm_model_workspace_size(C.byref(self.dims))
         self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=self.dev)
         v = layout.views
@@ -66,6 +66,11 @@ class ModelRunner:
         prm.g_emo_w = g32("emotion_head.weight")
         prm.g_capkv_w, prm.g_capkv_b = g32("__capkv_w"), g32("__capkv_b")
         prm.g_layer = C.c_void_p(gp + 4 * layout.layer_base[0])
+        if layout.Fd != E:
+            prm.vproj_w_b, prm.vproj_b = b16("transformer.visual_proj.weight"), f32("transformer.visual_proj.bias")
+            prm.aproj_w_b, prm.aproj_b = b16("transformer.audio_proj.weight"), f32("transformer.audio_proj.bias")
+            prm.g_vproj_w, prm.g_vproj_b = g32("transformer.visual_proj.weight"), g32("transformer.visual_proj.bias")
+            prm.g_aproj_w, prm.g_aproj_b = g32("transformer.audio_proj.weight"), g32("transformer.audio_proj.bias")
         self._params = prm  # keep alive
         plan = C.c_void_p()
         L.check(self.lib.ergm_model_create(C.byref(self.dims), C.byref(prm), _p(self.workspace), ws_bytes,

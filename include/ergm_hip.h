@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 1
+#define ERGM_ABI_VERSION 2
 
 typedef enum {
     ERGM_OK = 0,
@@ -198,7 +198,10 @@ typedef struct {
     int batch, seq;           /* local (per-rank) batch and sequence length */
     float eps;
     int has_features;         /* visual/audio injection present */
-    int ld_vis;               /* row stride of the visual feature (Tv*E when [B,Tv,E]) */
+    int ld_vis;               /* row stride of the visual feature (Tv*Fd when [B,Tv,Fd]) */
+    int feat_dim;             /* Fd: width of the pooled features; 0 or n_embd = added directly
+                               * (src/model.py:497-498); otherwise a Conv1D projection per modality
+                               * (build-side, config 5: 768-d features into a 1024-d backbone) */
 } ergm_model_dims;
 
 /* Pointer table: names follow the reference state_dict; see ergm_amd/model.py. */
@@ -217,6 +220,10 @@ typedef struct {
     /* gradients (f32, same layout as params) */
     float* g_wte; float* g_wpe; float* g_ln_f_w; float* g_ln_f_b; float* g_emo_w;
     float* g_capkv_w; float* g_capkv_b; float* g_layer;
+    /* feature projections (feat_dim != n_embd only): visual / audio Conv1D weights [Fd][E] (bf16
+     * shadow), biases [E] f32, gradients f32; each bias stored right after its weight */
+    const void* vproj_w_b; const float* vproj_b; const void* aproj_w_b; const float* aproj_b;
+    float* g_vproj_w; float* g_vproj_b; float* g_aproj_w; float* g_aproj_b;
 } ergm_model_params;
 
 typedef enum {

@@ -49,10 +49,20 @@ class OracleConfig:
     layer_norm_epsilon: float = 1e-5
     initializer_range: float = 0.02
     n_inner: Optional[int] = None
+    # Width of the pooled audio / visual features.  None (or == n_embd) is the reference model, which
+    # adds the features to the embeddings directly (src/model.py:497-498 requires width == n_embd).
+    # Otherwise a build-side Conv1D projection per modality maps feat_dim -> n_embd first (config 5:
+    # 768-d BLIP / wav2vec2 features into the 1024-d GPT-2-medium stream).  The
+    # projection has no reference counterpart: its parity is against this restatement only.
+    feat_dim: Optional[int] = None
 
     @property
     def inner(self) -> int:
         return self.n_inner if self.n_inner is not None else 4 * self.n_embd
+
+    @property
+    def projected(self) -> bool:
+        return self.feat_dim is not None and self.feat_dim != self.n_embd
 
 
 def param_shapes(cfg: OracleConfig) -> Dict[str, tuple]:
@@ -87,6 +97,10 @@ def param_shapes(cfg: OracleConfig) -> Dict[str, tuple]:
     s["transformer.ln_f.weight"] = (E,)
     s["transformer.ln_f.bias"] = (E,)
     s["emotion_head.weight"] = (NUM_EMOTIONS, E)
+    if cfg.projected:  # build-side feature projections (not in the reference state_dict)
+        for m in ("visual_proj", "audio_proj"):
+            s[f"transformer.{m}.weight"] = (cfg.feat_dim, E)
+            s[f"transformer.{m}.bias"] = (E,)
     return s
 
 
@@ -176,9 +190,13 @@ def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type
     enc_mask = torch.zeros(B, 1, 1, caption_embeds.shape[1])                  # :484-489 invert(ones)
     if visual_feat is not None:                                               # :495-498
         vis = visual_feat if visual_feat.dim() == 2 else visual_feat[:, 0]
+        aud = audio_feat
+        if cfg.projected:                                                     # build-side, config 5
+            vis = _conv1d(vis, P["transformer.visual_proj.weight"], P["transformer.visual_proj.bias"])
+            aud = _conv1d(aud, P["transformer.audio_proj.weight"], P["transformer.audio_proj.bias"])
         add = torch.zeros_like(inputs_embeds)
         add[:, 0] = vis
-        add[:, 1] = audio_feat
+        add[:, 1] = aud
         inputs_embeds = inputs_embeds + add
     pos = F.embedding(torch.arange(S), wpe)                                   # :474-476,500
     h = inputs_embeds + pos                                                   # :501

@@ -1,0 +1,75 @@
+"""Config 5 (BASELINE.json configs[4]) on the GPU: GPT-2-medium geometry (E=1024, H=16, d=64) with 768-d
+pooled visual / audio features entering through the build-side projection GEMMs (the
+reference adds features of width n_embd directly and has no projection; the projection's parity is
+against the oracle restatement, "parity unpinned" by the reference itself).
+
+bf16 gates as in test_gpu_model.py.
+"""
+import pytest
+import torch
+
+from ergm_amd.config import ERGMConfig
+from ergm_amd.data import synthetic_batch
+from ergm_amd.model import GPT2LMHeadModel
+from oracle import gpt2_oracle as O
+from test_gpu_model import LOSS_RTOL, LOGIT_ATOL, _grad_gate, _grads, _run
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(V, E, Lyr, H, Fd, seed):
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, feat_dim=Fd)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, feat_dim=Fd)
+    P0 = O.init_params(ocfg, seed=seed)
+    return ocfg, cfg, P0
+
+
+@pytest.mark.parametrize("vis_rows", [1, 4])
+def test_feature_projection_matches_oracle(gpu, vis_rows):
+    V, E, Lyr, H, Fd = 500, 128, 2, 2, 64
+    ocfg, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=21)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    batch = synthetic_batch(3, 64, n_turns=4, feat_dim=Fd, seed=4, vocab_hi=490, sp1=498, sp2=499, eos=489,
+                            visual_rows=vis_rows)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    assert abs(out.loss.item() - ref["loss"].item()) <= LOSS_RTOL * abs(ref["loss"].item())
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    g = _grads(model)
+    assert set(g) == set(og)
+    _grad_gate(g, og)
+    # the projections really receive gradient (features reach positions 0 and 1 through them)
+    for m in ("visual_proj", "audio_proj"):
+        assert og[f"transformer.{m}.weight"].norm() > 0 and g[f"transformer.{m}.bias"].norm() > 0
+
+
+def test_text_only_batch_through_projected_model(gpu):
+    V, E, Lyr, H, Fd = 500, 128, 1, 2, 64
+    ocfg, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=22)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    batch = synthetic_batch(2, 32, n_turns=3, feat_dim=Fd, seed=5, vocab_hi=490, sp1=498, sp2=499, eos=489)
+    batch.pop("visual_feat"), batch.pop("audio_feat")
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    assert abs(out.loss.item() - ref["loss"].item()) <= LOSS_RTOL * abs(ref["loss"].item())
+    g = _grads(model)
+    assert g["transformer.visual_proj.weight"].abs().max().item() == 0.0
+    _grad_gate(g, og)
+
+
+def test_gpt2_medium_geometry_with_768d_features(gpu):
+    """E=1024, H=16 (two of the 24 blocks, to keep the CPU oracle at seconds), full vocabulary,
+    768-d features projected to 1024, MELD shape S=128."""
+    V, E, Lyr, H, Fd = 50260, 1024, 2, 16, 768
+    ocfg, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=23)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    batch = synthetic_batch(2, 128, n_turns=5, feat_dim=Fd, seed=6)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    assert abs(out.loss.item() - ref["loss"].item()) <= LOSS_RTOL * abs(ref["loss"].item())
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    assert (out.emotion_logits.cpu() - ref["emotion_logits"]).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), og)
