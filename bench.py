@@ -44,11 +44,13 @@ def pmc_traffic(probe: int, config: str = "c2"):
         return None, None
     return round(rec["hbm_bytes"]), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {
-    # name: (model, S, turns, batch per GPU, pooled feature width, description)
-    "c2": ("small", 128, 5, 16, 768, "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
-    "c4": ("small", 512, 20, 8, 768, "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
-    "c5": ("medium", 128, 5, 32, 768, "GPT-2-medium + 768-d audio/visual features through projection GEMMs, "
-           "MELD-shape (S=128, 5 turns), B=32/GPU"),
+    # name: (model, S, turns, batch per GPU, pooled feature width, fp8 forward GEMMs, description)
+    "c2": ("small", 128, 5, 16, 768, False,
+           "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
+    "c4": ("small", 512, 20, 8, 768, False,
+           "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
+    "c5": ("medium", 128, 5, 32, 768, True, "GPT-2-medium + 768-d audio/visual features through projection "
+           "GEMMs, fp8 (e4m3) forward Conv1D GEMMs, MELD-shape (S=128, 5 turns), B=32/GPU"),
 }
 MODELS = {"small": dict(n_embd=768, n_layer=12, n_head=12), "medium": dict(n_embd=1024, n_layer=24, n_head=16)}
 
@@ -99,6 +101,7 @@ def main():
     ap.add_argument("--adamw-blocks", type=int, default=None,
                     help="grid cap of the overlapped per-bucket AdamW (default: FusedAdamW.overlap_blocks)")
     ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
+    ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,8 +124,11 @@ def main():
     from ergm_amd.model import GPT2LMHeadModel
     from ergm_amd.optim import FusedAdamW, get_polynomial_decay_schedule_with_warmup
 
-    mname, S, turns, B, Fd, desc = CONFIGS[args.config]
-    cfg = ERGMConfig(**MODELS[mname], feat_dim=Fd)
+    mname, S, turns, B, Fd, fp8, desc = CONFIGS[args.config]
+    fp8 = fp8 and not args.no_fp8
+    if not fp8:
+        desc = desc.replace("fp8 (e4m3) forward Conv1D GEMMs", "bf16 GEMMs")
+    cfg = ERGMConfig(**MODELS[mname], feat_dim=Fd, fp8=fp8)
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
@@ -206,7 +212,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8e4m3 fwd GEMMs + bf16" if fp8 else "bf16",
         "data": f"synthetic (seeded MELD-shape token/feature batches; random-init GPT-2-{mname} weights)",
         "config": {"workload": desc, "model": f"GPT-2-{mname} (L={Lyr}, E={E}, H={cfg.n_head}, V={V}) + "
                    "cross-attention caption fusion + emotion head", "global_batch": B * world, "seq_len": S,

@@ -37,7 +37,7 @@ class ModelDims(C.Structure):
     _fields_ = [("vocab", C.c_int), ("vocab_pad", C.c_int), ("n_embd", C.c_int), ("n_layer", C.c_int),
                 ("n_head", C.c_int), ("n_inner", C.c_int), ("n_positions", C.c_int), ("batch", C.c_int),
                 ("seq", C.c_int), ("eps", C.c_float), ("has_features", C.c_int), ("ld_vis", C.c_int),
-                ("feat_dim", C.c_int)]
+                ("feat_dim", C.c_int), ("fp8", C.c_int)]
 
 
 class ModelParams(C.Structure):
@@ -50,7 +50,7 @@ class ModelParams(C.Structure):
                 ("g_layer", C.c_void_p),
                 ("vproj_w_b", C.c_void_p), ("vproj_b", C.c_void_p), ("aproj_w_b", C.c_void_p),
                 ("aproj_b", C.c_void_p), ("g_vproj_w", C.c_void_p), ("g_vproj_b", C.c_void_p),
-                ("g_aproj_w", C.c_void_p), ("g_aproj_b", C.c_void_p)]
+                ("g_aproj_w", C.c_void_p), ("g_aproj_b", C.c_void_p), ("capkv_w", C.c_void_p)]
 
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
@@ -60,6 +60,10 @@ _SIGS = {
     "ergm_gemm_tune": (i32, [i32, i32]),
     "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
+    "ergm_gemm_f8": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, vp, vp]),
+    "ergm_gemm_f8_tune": (i32, [i32]),
+    "ergm_quant_rows_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp]),
+    "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp]),
     "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "ergm_attn_tune": (i32, [i32]),
     "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),

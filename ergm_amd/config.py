@@ -37,6 +37,9 @@ class ERGMConfig:
     # width of the pooled audio / visual features (data_process/feature_extraction.py:63,69 → 768).
     # When it differs from n_embd a build-side projection GEMM maps it (config 5).
     feat_dim: Optional[int] = None
+    # config 5: forward Conv1D GEMMs on fp8 (e4m3, per-row activation / per-column weight scales,
+    # block-scaled MFMA at 2x the bf16 rate); LM head, backward and optimizer stay bf16 / fp32
+    fp8: bool = False
 
     @property
     def inner(self) -> int:

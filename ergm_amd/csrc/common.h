@@ -45,6 +45,20 @@ __device__ __forceinline__ __bf16 f2bf(float x) { return (__bf16)x; }  // RNE (v
 
 __device__ __forceinline__ float bits2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
+// fp8 weight quantisation jobs (quant.hip), batched over the matrices of one block
+struct WqJob {
+    const float* W;       // [K][ldw] f32 (Conv1D [in, out])
+    uint8_t* Wt;          // [N][ldt] e4m3 (transposed)
+    float* scale;         // [N]
+    unsigned* amax;       // [N] |w| bit patterns, zeroed by the caller
+    int ldw, K, N, ldt;
+    int blk_amax, blk_q;  // first block of this job in each grid (set by quant_weights_fp8)
+};
+struct WqJobs {
+    WqJob j[8];
+    int n;
+};
+
 // wave-level reductions over 64 lanes
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

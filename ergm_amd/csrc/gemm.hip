@@ -12,6 +12,7 @@
 // m/n-contiguous tiles are read column-wise with ds_read_b64_tr_b16 (CDNA4 transpose read) under a
 // row-dependent chunk XOR that keeps each 32-lane half conflict-free.
 #include <algorithm>
+#include <cstring>
 
 #include "common.h"
 
@@ -37,6 +38,8 @@ struct GemmArgs {
     int sweep_m;        // 1: consecutive tile ids walk M (B panel reused), 0: walk N
     int k_per_split;    // K range per blockIdx.z (multiple of 64)
     float* slab;        // split-K partials [z][M][N] (f32) or nullptr
+    const float* a_scale;  // fp8 GEMM: per-row dequantisation scale of A [M] (nullptr: none)
+    const float* b_scale;  // fp8 GEMM: per-column dequantisation scale of B [N]
 };
 
 // XOR swizzles (chunk = 16 bytes).
@@ -193,7 +196,8 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
 // global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
 // (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
 // the staging buffer is (BM/WGM)*(BN+4) floats.  slab != nullptr: raw f32 split-K partials.
-template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN>
+template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN,
+          bool RS = false>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
                                            float alpha, float* slab) {
     // NT: every thread of the workgroup (a warp-specialised kernel adds producer waves, which only
@@ -230,6 +234,14 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
             } else {
                 float v[8] = {x0.x * alpha, x0.y * alpha, x0.z * alpha, x0.w * alpha,
                               x1.x * alpha, x1.y * alpha, x1.z * alpha, x1.w * alpha};
+                if constexpr (RS) {  // fp8 dequantisation: row scale of A times column scale of B
+                    const float sa = a.a_scale[m];
+                    const float4 b0 = *reinterpret_cast<const float4*>(a.b_scale + n);
+                    const float4 b1 = *reinterpret_cast<const float4*>(a.b_scale + n + 4);
+                    const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] *= sa * sb[j];
+                }
                 epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
             }
         }
@@ -560,6 +572,92 @@ __global__ __launch_bounds__(64 * (WGM * WGN + NP)) void gemm_ws_kernel(GemmArgs
     store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * (NC + NP)>(a, smem, acc, m0, n0, alpha, slab);
 }
 
+// ------------------------------------------------------------------------------------------
+// fp8 (OCP e4m3fn) GEMM for the config-5 forward: A [M][K] and B [N][K] bytes (k contiguous: the
+// activations as produced, the weights stored transposed by ergm_quant_weight_fp8), one
+// v_mfma_scale_f32_16x16x128_f8f6f4 per 16x16 output fragment per 128-deep K step with unit block
+// scales (e8m0 127 = 2^0) — the block-scaled instruction runs e4m3 at twice the bf16 MFMA rate, the
+// unscaled fp8 forms only at the bf16 rate (MI355X_MICROARCH.md, matrix cores).  Dequantisation by the
+// per-row scale of A and per-column scale of B happens once, in the epilogue.
+// A 128-byte K step has the byte layout of the bf16 kernels' 64-element step, so the same LDS-DMA
+// ring (GldsTile on a 2-byte view) and XOR swizzle stage it; lane l reads the 32 bytes of row l&15 at
+// k-offset 32·(l>>4) (two 16-B chunks).
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+template <int ROWS>
+__device__ __forceinline__ i32x8 frag_f8(const char* lds, int ro) {
+    const int lane = threadIdx.x & 63;
+    const int row = ro + (lane & 15), g = lane >> 4;
+    const char* base = lds + row * 128;
+    const int sw = swz_row(row);
+    const uint4 lo = *reinterpret_cast<const uint4*>(base + (((2 * g) ^ sw) << 4));
+    const uint4 hi = *reinterpret_cast<const uint4*>(base + (((2 * g + 1) ^ sw) << 4));
+    return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmArgs a) {
+    constexpr int NW = WGM * WGN;
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+    constexpr int STAGE = A_BYTES + B_BYTES;
+    constexpr int LPS = GldsTile<BM, false, NW>::PER_WAVE + GldsTile<BN, false, NW>::PER_WAVE;
+    static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int id = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int nk = a.K / 128;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave / WGN, wn = wave % WGN;
+    // 2-byte views: a 128-byte K step is "64 elements" of the bf16 staging code
+    const __bf16* A2 = a.A;
+    const __bf16* B2 = a.B;
+    const int lda2 = a.lda / 2, ldb2 = a.ldb / 2;
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_stage = [&](int kt) {
+        char* st = smem + (kt % NS) * STAGE;
+        const int k0 = kt * 64;
+        GldsTile<BM, false, NW>::issue(st, A2, lda2, m0, a.M, k0, wave);
+        GldsTile<BN, false, NW>::issue(st + A_BYTES, B2, ldb2, n0, a.N, k0, wave);
+    };
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue_stage(s);
+    for (int kt = 0; kt < nk; ++kt) {
+        wait_stages<LPS, NS - 2>(min(NS - 2, nk - 1 - kt));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+        const char* st = smem + (kt % NS) * STAGE;
+        i32x8 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = frag_f8<BM>(st, wm * WM + i * 16);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = frag_f8<BN>(st + A_BYTES, wn * WN + j * 16);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                              127);
+    }
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * NW, true>(a, smem, acc, m0, n0, alpha, nullptr);
+}
+
 // split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
 template <int EPI, bool OUT_BF16>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int splits) {
@@ -788,6 +886,109 @@ static void launch_reduce(const GemmArgs& a, int split, hipStream_t s) {
 
 using namespace ergm;
 
+namespace ergm {
+// fp8 configurations (tile, wave grid, stages); a stage is (BM + BN) x 128 bytes
+struct F8Cfg {
+    int bm, bn, wgm, wgn, ns;
+};
+static constexpr F8Cfg kF8Cfgs[] = {
+    {128, 128, 2, 2, 3},  // 0
+    {256, 128, 4, 2, 3},  // 1  8 waves
+    {128, 128, 4, 2, 3},  // 2  8 waves (32x64 each)
+    {256, 256, 4, 2, 2},  // 3  8 waves (64x128 each)
+    {64, 64, 2, 2, 4},    // 4
+};
+static constexpr int kNumF8Cfgs = sizeof(kF8Cfgs) / sizeof(kF8Cfgs[0]);
+static thread_local int g_force_f8_cfg = -1;
+
+template <int C, int EPI, bool OB>
+static void launch_f8_cfg(const GemmArgs& a, hipStream_t s) {
+    constexpr F8Cfg c = kF8Cfgs[C];
+    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * 128, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
+    auto k = gemm_f8_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, EPI, OB>;
+    static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
+    (void)attr;
+    hipLaunchKernelGGL(k, dim3(a.tiles_m * a.tiles_n), dim3(64 * c.wgm * c.wgn), lds, s, a);
+}
+
+template <int EPI, bool OB>
+static void launch_f8(const GemmArgs& a, int cfg, hipStream_t s) {
+    switch (cfg) {
+        case 0: launch_f8_cfg<0, EPI, OB>(a, s); break;
+        case 1: launch_f8_cfg<1, EPI, OB>(a, s); break;
+        case 2: launch_f8_cfg<2, EPI, OB>(a, s); break;
+        case 3: launch_f8_cfg<3, EPI, OB>(a, s); break;
+        default: launch_f8_cfg<4, EPI, OB>(a, s); break;
+    }
+}
+
+static int plan_f8(int M, int N) {
+    if (g_force_f8_cfg >= 0) return g_force_f8_cfg;
+    const long t128 = tiles_of(M, N, 128, 128);
+    if (t128 >= 4000) return 3;
+    if (t128 >= 512) return 1;
+    if (t128 >= 140) return 2;
+    return 4;
+}
+
+}  // namespace ergm
+
+extern "C" int ergm_gemm_f8_tune(int cfg) {
+    ERGM_CHECK_ARG(cfg >= -1 && cfg < ergm::kNumF8Cfgs, "gemm_f8_tune: cfg in [-1, %d)", ergm::kNumF8Cfgs);
+    ergm::g_force_f8_cfg = cfg;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_gemm_f8(const ergm_gemm_desc* d, const void* A, const float* a_scale, const void* B,
+                            const float* b_scale, void* C, void* stream) {
+    using namespace ergm;
+    ERGM_CHECK_ARG(d && A && B && C && a_scale && b_scale, "ergm_gemm_f8: null argument");
+    ERGM_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0 && d->K % 128 == 0, "ergm_gemm_f8: K=%d must be a multiple of 128",
+                   d->K);
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK && d->b_layout == ERGM_NK, "ergm_gemm_f8: A [M][K] and B [N][K] only");
+    ERGM_CHECK_ARG(d->lda >= d->K && d->ldb >= d->K && d->lda % 16 == 0 && d->ldb % 16 == 0,
+                   "ergm_gemm_f8: lda/ldb >= K, multiples of 16 bytes");
+    ERGM_CHECK_ARG(aligned16(A) && aligned16(B) && aligned16(b_scale), "ergm_gemm_f8: 16-byte alignment");
+    ERGM_CHECK_ARG(d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldc >= d->N, "ergm_gemm_f8: N, ldc multiples of 8");
+    ERGM_CHECK_ARG(d->c_dtype == ERGM_F32 || d->c_dtype == ERGM_BF16, "ergm_gemm_f8: bad c_dtype");
+    const int e = d->epilogue;
+    ERGM_CHECK_ARG((e == ERGM_EPI_NONE || e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) ? d->c_dtype == ERGM_BF16 ||
+                       e == ERGM_EPI_NONE
+                                                                                        : e == ERGM_EPI_BIAS_RESID &&
+                                                                                              d->c_dtype == ERGM_F32,
+                   "ergm_gemm_f8: epilogue %d with c_dtype %d not supported", e, d->c_dtype);
+    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_RESID || (d->aux && d->ld_aux % 8 == 0), "ergm_gemm_f8: residual needs aux");
+    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || (d->aux_out && d->ld_aux_out % 8 == 0), "ergm_gemm_f8: GELU needs aux_out");
+    const int cfg = plan_f8(d->M, d->N);
+    GemmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = reinterpret_cast<const __bf16*>(A);
+    a.B = reinterpret_cast<const __bf16*>(B);
+    a.C = C;
+    a.M = d->M; a.N = d->N; a.K = d->K;
+    a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+    a.alpha = d->alpha; a.alpha_dev = d->alpha_dev;
+    a.bias = d->bias; a.aux = d->aux; a.ld_aux = d->ld_aux;
+    a.aux_out = d->aux_out; a.ld_aux_out = d->ld_aux_out;
+    a.tiles_m = cdiv(d->M, kF8Cfgs[cfg].bm);
+    a.tiles_n = cdiv(d->N, kF8Cfgs[cfg].bn);
+    a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
+    a.a_scale = a_scale;
+    a.b_scale = b_scale;
+    hipStream_t s = as_stream(stream);
+    const bool ob = d->c_dtype == ERGM_BF16;
+    switch (e) {
+        case ERGM_EPI_NONE:
+            if (ob) launch_f8<ERGM_EPI_NONE, true>(a, cfg, s);
+            else launch_f8<ERGM_EPI_NONE, false>(a, cfg, s);
+            break;
+        case ERGM_EPI_BIAS: launch_f8<ERGM_EPI_BIAS, true>(a, cfg, s); break;
+        case ERGM_EPI_BIAS_GELU: launch_f8<ERGM_EPI_BIAS_GELU, true>(a, cfg, s); break;
+        default: launch_f8<ERGM_EPI_BIAS_RESID, false>(a, cfg, s); break;
+    }
+    return check_launch("ergm_gemm_f8");
+}
+
 extern "C" int ergm_gemm_tune(int cfg, int split) {
     ERGM_CHECK_ARG(cfg >= -1 && cfg < kNumCfgs && split >= 0, "gemm_tune: cfg in [-1, %d), split >= 0", kNumCfgs);
     g_force_cfg = cfg;
@@ -840,6 +1041,7 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
     a.k_per_split = p.kps;
     a.slab = nullptr;
+    a.a_scale = a.b_scale = nullptr;
     hipStream_t s = as_stream(stream);
     if (p.split > 1) {
         size_t need = (size_t)p.split * d->M * d->N * sizeof(float);

@@ -24,7 +24,10 @@ using namespace ergm;
 
 namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
-                     int rows, int E, float eps, hipStream_t s);
+                     int rows, int E, float eps, hipStream_t s, void* yq = nullptr, int ldq = 0, float* qscale = nullptr);
+int quant_weights_fp8(const WqJobs& J, hipStream_t s);
+int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
+                   hipStream_t s);
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
@@ -49,6 +52,15 @@ struct LayerActs {
     float *m1, *r1, *mx, *rx, *m2, *r2;
     __bf16 *qkv, *ao, *xq, *xo, *pre, *act;
     float *lse, *xlse;
+};
+
+// fp8 (config 5) copies of one block's six Conv1D weights, transposed to [N][K] e4m3 with per-column
+// scales (order: c_attn, attn c_proj, q_attn, cross c_proj, c_fc, mlp c_proj), and their amax scratch
+struct LayerW8 {
+    uint8_t* w[6];
+    float* sc[6];
+    unsigned* amax;
+    int amax_n;
 };
 
 struct ergm_model_plan {
@@ -77,6 +89,15 @@ struct ergm_model_plan {
     __bf16* feat_b16;
     float* proj_out;
     __bf16* dproj;
+    // fp8 forward (dims.fp8): per-block weight copies re-quantised at every forward on the side stream
+    // (ev_wq[l] marks block l's), the caption K/V weights likewise, and the transient row-quantised
+    // activations (main stream: one buffer reused block after block; side stream: the captions)
+    bool f8;
+    std::vector<LayerW8> w8;
+    uint8_t *capkv8, *qa, *qf, *qcap;
+    float *capkv8_s, *sa, *sf, *scap;
+    unsigned* capkv_amax;
+    std::vector<hipEvent_t> ev_wq;
     // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
@@ -164,6 +185,34 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->emo_sum = c.take<float>(4);
     P->emo_tmp = c.take<float>((size_t)d.batch * 16 + 8);
     P->n_valid_local = c.take<int>(4);
+    P->f8 = d.fp8 != 0;
+    P->w8.assign(P->f8 ? L : 0, LayerW8{});
+    P->capkv8 = P->qa = P->qf = P->qcap = nullptr;
+    P->capkv8_s = P->sa = P->sf = P->scap = nullptr;
+    P->capkv_amax = nullptr;
+    if (P->f8) {
+        const size_t KN[6][2] = {{E, 3 * E}, {E, E}, {E, E}, {E, E}, {E, F}, {F, E}};
+        for (size_t l = 0; l < L; ++l) {
+            LayerW8& w = P->w8[l];
+            int na = 0;
+            for (int i = 0; i < 6; ++i) {
+                w.w[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
+                w.sc[i] = c.take<float>(KN[i][1]);
+                na += (int)KN[i][1];
+            }
+            w.amax = c.take<unsigned>(na);
+            w.amax_n = na;
+        }
+        P->capkv8 = c.take<uint8_t>((size_t)2 * E * L * E);
+        P->capkv8_s = c.take<float>((size_t)2 * E * L);
+        P->capkv_amax = c.take<unsigned>((size_t)2 * E * L);
+        P->qa = c.take<uint8_t>(T * E);
+        P->sa = c.take<float>(T);
+        P->qf = c.take<uint8_t>(T * F);
+        P->sf = c.take<float>(T);
+        P->qcap = c.take<uint8_t>(T * E);
+        P->scap = c.take<float>(T);
+    }
     P->Fd = d.feat_dim > 0 ? d.feat_dim : (int)E;
     P->proj = d.has_features && P->Fd != (int)E;
     P->Bp = (d.batch + 63) / 64 * 64;
@@ -219,6 +268,19 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
     if (P->dry) return ERGM_OK;
     char* ws = (s != nullptr && s == P->side) ? P->scratch2 : P->scratch;
     return ergm_gemm(&g, A, B, C, ws, P->scratch_bytes, s);
+}
+
+// fp8 forward GEMM: C[M][N] = epi(sa[m]·sb[n]·A8[m][:]·B8t[n][:]) (both operands k-contiguous, K bytes)
+int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* Bt,
+          const float* sb, void* C, int ldc, int cdt, int epi, const float* bias, const void* aux = nullptr,
+          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0) {
+    if (P->dry) return ERGM_OK;
+    ergm_gemm_desc g;
+    memset(&g, 0, sizeof(g));
+    g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = ldc;
+    g.a_layout = ERGM_MK; g.b_layout = ERGM_NK; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
+    g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
+    return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
 }
 
 int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, int cols, int ldx, float* out) {
@@ -310,6 +372,26 @@ inline float* LG(const ergm_model_plan* P, int l, int t) {
     return P->p.g_layer + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
 }
 
+// Re-quantise block l's six Conv1D weights (f32 master → transposed e4m3 + column scales) on `ss` and
+// mark ev_wq[l]; the block's forward waits for that mark.
+int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
+    if (P->dry) return ERGM_OK;
+    const int E = P->d.n_embd, F = P->d.n_inner;
+    LayerW8& w = P->w8[l];
+    if (hipMemsetAsync(w.amax, 0, (size_t)w.amax_n * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "model: memset");
+    const int tens[6] = {ERGM_T_ATTN_W, ERGM_T_APROJ_W, ERGM_T_XQ_W, ERGM_T_XPROJ_W, ERGM_T_FC_W, ERGM_T_MPROJ_W};
+    const int K[6] = {E, E, E, E, E, F}, N[6] = {3 * E, E, E, E, F, E};
+    WqJobs J{};
+    J.n = 6;
+    unsigned* am = w.amax;
+    for (int i = 0; i < 6; ++i) {
+        J.j[i] = WqJob{LF(P, l, tens[i]), w.w[i], w.sc[i], am, N[i], K[i], N[i], K[i], 0, 0};
+        am += N[i];
+    }
+    ERGM_TRY(quant_weights_fp8(J, ss));
+    return hipEventRecord(P->ev_wq[l], ss) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: event record");
+}
+
 int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s);
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s);
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s);
@@ -350,6 +432,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     ERGM_CHECK_ARG((d.batch * d.seq) % 8 == 0, "model_create: B*S must be a multiple of 8");
     ERGM_CHECK_ARG(d.n_layer > 0, "model_create: n_layer must be > 0");
     ERGM_CHECK_ARG(d.feat_dim >= 0 && d.feat_dim % 64 == 0, "model_create: feat_dim must be a multiple of 64");
+    ERGM_CHECK_ARG(!d.fp8 || (d.n_embd % 128 == 0 && d.n_inner % 128 == 0 && params->capkv_w),
+                   "model_create: fp8 needs n_embd, n_inner multiples of 128 and the f32 caption K/V weight");
     if (d.has_features && d.feat_dim > 0 && d.feat_dim != d.n_embd) {
         const ergm_model_params& q = *params;
         ERGM_CHECK_ARG(q.vproj_w_b && q.vproj_b && q.aproj_w_b && q.aproj_b && q.g_vproj_w && q.g_aproj_w,
@@ -377,6 +461,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
+    P->ev_wq.assign(P->f8 ? d.n_layer : 0, nullptr);
+    for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
         ergm_model_destroy(P);
         return fail(ERGM_EHIP, "model_create: stream/event creation failed");
@@ -427,6 +513,8 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
     if (!P) return ERGM_OK;
     if (P->side) hipStreamSynchronize(P->side);
     for (auto e : P->ev_join)
+        if (e) hipEventDestroy(e);
+    for (auto e : P->ev_wq)
         if (e) hipEventDestroy(e);
     if (P->ev_fork) hipEventDestroy(P->ev_fork);
     if (P->side) hipStreamDestroy(P->side);
@@ -503,13 +591,30 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
+        if (P->f8) ERGM_TRY(quant_layer_weights(P, 0, ss));
         // the embedding backward's sort needs only the ids: done here, off the critical chain
         if (train && !P->dry)
             ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
-        Probe pr(P, 4, ss);
-        ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E, ERGM_BF16,
-                      ERGM_EPI_BIAS, p.capkv_b));
+        if (P->f8 && !P->dry) {
+            if (hipMemsetAsync(P->capkv_amax, 0, (size_t)L2E * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "memset");
+            WqJobs J{};
+            J.n = 1;
+            J.j[0] = WqJob{p.capkv_w, P->capkv8, P->capkv8_s, P->capkv_amax, L2E, E, L2E, E, 0, 0};
+            ERGM_TRY(quant_weights_fp8(J, ss));
+            ERGM_TRY(quant_rows_fp8(P->cap, ERGM_BF16, P->XE, T, E, P->qcap, E, P->scap, ss));
+        }
+        {
+            Probe pr(P, 4, ss);
+            if (P->f8)
+                ERGM_TRY(gemm8(P, ss, T, L2E, E, P->qcap, P->scap, P->capkv8, P->capkv8_s, P->kv_all, L2E, ERGM_BF16,
+                               ERGM_EPI_BIAS, p.capkv_b));
+            else
+                ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E,
+                              ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b));
+        }
         ERGM_TRY(side_mark(P, L));
+        if (P->f8)
+            for (int l = 1; l < L; ++l) ERGM_TRY(quant_layer_weights(P, l, ss));
     }
     for (int l = 0; l < L; ++l) {
         LayerActs& a = P->la[l];
@@ -517,37 +622,72 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         float* x1 = P->resid[3 * l + 1];
         float* x2 = P->resid[3 * l + 2];
         float* x3 = P->resid[3 * l + 3];
+        // fp8 (config 5): every Conv1D below consumes row-quantised activations (the LayerNorms write
+        // their fp8 copy themselves, attention / GELU outputs go through quant_rows_fp8) and block l's
+        // re-quantised weights, which the side stream marks ready with ev_wq[l]
+        const bool f8 = P->f8;
+        const LayerW8* w8 = f8 && !P->dry ? &P->w8[l] : nullptr;
+        uint8_t* qa = f8 ? P->qa : nullptr;
+        if (w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
         // self-attention sub-block (src/model.py:297-309)
         if (!P->dry)
             ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
-                                      d.eps, s));
-        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
-                      ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+                                      d.eps, s, qa, E, P->sa));
+        if (f8)
+            ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, P->sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
+                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+        else
+            ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
+                          ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
         if (!P->dry)
             ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
                                    s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+        if (f8) {
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, P->sa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
+                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+        } else {
+            ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+        }
         // cross-attention over caption embeddings (src/model.py:311-329)
         if (!P->dry)
             ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
-                                      d.eps, s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
-                      ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+                                      d.eps, s, qa, E, P->sa));
+        if (f8)
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E,
+                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+        else
+            ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
+                          ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
         if (l == 0) ERGM_TRY(join_side(P, s, L));
         if (!P->dry)
             ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, P->XE, 0, s));
-        ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+        if (f8) {
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, P->sa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
+                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+        } else {
+            ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+        }
         // MLP (src/model.py:331-334, 262-267)
         if (!P->dry)
             ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
-                                      d.eps, s));
-        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF, ERGM_BF16,
-                      ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-        ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+                                      d.eps, s, qa, E, P->sa));
+        if (f8) {
+            ERGM_TRY(gemm8(P, s, T, F, E, qa, P->sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
+                           ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, P->qf, F, P->sf, s));
+            ERGM_TRY(gemm8(P, s, T, E, F, P->qf, P->sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E,
+                           ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+        } else {
+            ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF,
+                          ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+            ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+        }
     }
     if (!P->dry)
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));

@@ -16,7 +16,8 @@ template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, __bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int rows, int E, int ldy, float eps) {
+                                                     int rows, int E, int ldy, float eps, uint8_t* __restrict__ yq,
+                                                     int ldq, float* __restrict__ qscale) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;
@@ -46,18 +47,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     }
     const float var = wave_sum(q) * inv_e;
     const float rstd = 1.0f / sqrtf(var + eps);
+    float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         int c = (i * 64 + lane) * 4;
         if (c < E) {
             const float4 g = gv[i], b = bv[i];
+            v[i].x = (v[i].x - mean) * rstd * g.x + b.x;
+            v[i].y = (v[i].y - mean) * rstd * g.y + b.y;
+            v[i].z = (v[i].z - mean) * rstd * g.z + b.z;
+            v[i].w = (v[i].w - mean) * rstd * g.w + b.w;
             bf16x4 o;
-            o[0] = f2bf((v[i].x - mean) * rstd * g.x + b.x);
-            o[1] = f2bf((v[i].y - mean) * rstd * g.y + b.y);
-            o[2] = f2bf((v[i].z - mean) * rstd * g.z + b.z);
-            o[3] = f2bf((v[i].w - mean) * rstd * g.w + b.w);
+            o[0] = f2bf(v[i].x);
+            o[1] = f2bf(v[i].y);
+            o[2] = f2bf(v[i].z);
+            o[3] = f2bf(v[i].w);
             *reinterpret_cast<bf16x4*>(y + (size_t)row * ldy + c) = o;
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
         }
+    }
+    if (yq) {  // fp8 copy for the config-5 forward GEMMs (row scale, quant.hip's scheme)
+        amax = wave_max(amax);
+        const float sc = amax > 0.f ? amax / 448.f : 1.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            int c = (i * 64 + lane) * 4;
+            if (c < E) {
+                float a = fminf(fmaxf(v[i].x / sc, -448.f), 448.f), b = fminf(fmaxf(v[i].y / sc, -448.f), 448.f);
+                float cc = fminf(fmaxf(v[i].z / sc, -448.f), 448.f), d = fminf(fmaxf(v[i].w / sc, -448.f), 448.f);
+                int qq = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+                qq = __builtin_amdgcn_cvt_pk_fp8_f32(cc, d, qq, true);
+                *reinterpret_cast<int*>(yq + (size_t)row * ldq + c) = qq;
+            }
+        }
+        if (lane == 0) qscale[row] = sc;
     }
     if (lane == 0) {
         mean_out[row] = mean;
@@ -298,7 +321,9 @@ using namespace ergm;
 
 namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
-                     int rows, int E, float eps, hipStream_t s) {
+                     int rows, int E, float eps, hipStream_t s, void* yq, int ldq, float* qscale) {
+    ERGM_CHECK_ARG(!yq || (qscale && ldq >= E && ldq % 4 == 0), "layernorm_fwd: bad fp8 output");
+    auto* q8 = reinterpret_cast<uint8_t*>(yq);
     ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_fwd: unsupported E=%d", E);
     ERGM_CHECK_ARG(ldy >= E && ldy % 4 == 0, "layernorm_fwd: bad ldy");
@@ -306,10 +331,10 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
     int nv = cdiv(E, 256);
     auto* yb = reinterpret_cast<__bf16*>(y);
     switch (nv) {
-        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
-        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
-        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
-        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps); break;
+        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
     }
     return check_launch("layernorm_fwd");
 }
@@ -335,7 +360,7 @@ int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s) {
 
 extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
                                   float* rstd, int rows, int E, float eps, void* stream) {
-    return layernorm_fwd_ld(x, gamma, beta, y, E, mean, rstd, rows, E, eps, as_stream(stream));
+    return layernorm_fwd_ld(x, gamma, beta, y, E, mean, rstd, rows, E, eps, as_stream(stream), nullptr, 0, nullptr);
 }
 
 extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {

@@ -1,0 +1,178 @@
+// fp8 (OCP e4m3fn) quantisation for the config-5 forward GEMMs on gfx950 (BASELINE.json configs[4]:
+// "GPT-2-medium backbone + 3-modality fusion, fp8 MFMA weight path").  Build-side: the reference trains
+// in fp32 (src/main.py:62-68); SURVEY §8(c) states the fp8 tolerance.
+//
+// Scaling scheme (consumed by ergm_gemm_f8's epilogue):
+//   activations  per row    scale[r] = max_c |X[r][c]| / 448,  Q[r][c] = e4m3(X[r][c] / scale[r])
+//   weights      per output column of the Conv1D W[in][out]: scale[n] = max_k |W[k][n]| / 448, stored
+//                transposed Wt[n][k] so both GEMM operands are k-contiguous
+// 448 is the largest finite e4m3fn value; inputs are clamped to ±448 after the division so rounding can
+// never reach the NaN code.  A row / column of zeros gets scale 1.  HBM-bound, one pass per tensor
+// (weights: an amax pass and a quantise pass, both over L2-sized tiles).
+#include "common.h"
+
+namespace ergm {
+
+__device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d) {
+    a = fminf(fmaxf(a, -448.f), 448.f);
+    b = fminf(fmaxf(b, -448.f), 448.f);
+    c = fminf(fmaxf(c, -448.f), 448.f);
+    d = fminf(fmaxf(d, -448.f), 448.f);
+    int q = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    q = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, q, true);
+    return (uint32_t)q;
+}
+
+__device__ __forceinline__ uint8_t fp8x1(float a) {
+    a = fminf(fmaxf(a, -448.f), 448.f);
+    return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.f, 0, false) & 0xff);
+}
+
+__device__ __forceinline__ void load8(const void* X, bool bf16_in, size_t off, float* v) {
+    if (bf16_in) {
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(X) + off);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf2f(x[j]);
+    } else {
+        const float4 x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off);
+        const float4 x1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+        v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    }
+}
+
+// one row per wavefront; 8 consecutive columns per lane per pass (16-B bf16 / 32-B f32 loads)
+template <bool BF16_IN>
+__global__ __launch_bounds__(256) void quant_rows_kernel(const void* __restrict__ X, int ldx, int rows, int cols,
+                                                         uint8_t* __restrict__ Q, int ldq, float* __restrict__ scale) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;
+    const size_t base = (size_t)row * ldx;
+    float amax = 0.f;
+    for (int c = lane * 8; c < cols; c += 512) {
+        float v[8];
+        load8(X, BF16_IN, base + c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    }
+    amax = wave_max(amax);
+    const float s = amax > 0.f ? amax / 448.f : 1.f;
+    for (int c = lane * 8; c < cols; c += 512) {
+        float v[8];
+        load8(X, BF16_IN, base + c, v);
+        uint2 o;
+        o.x = fp8x4(v[0] / s, v[1] / s, v[2] / s, v[3] / s);
+        o.y = fp8x4(v[4] / s, v[5] / s, v[6] / s, v[7] / s);
+        *reinterpret_cast<uint2*>(Q + (size_t)row * ldq + c) = o;
+    }
+    if (lane == 0) scale[row] = s;
+}
+
+// ---- weights: batched over the matrices of one block (WqJobs in common.h) ------------------------
+
+__device__ __forceinline__ int find_job(const WqJobs& J, int bid, bool q) {
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+        if (i < J.n && bid >= (q ? J.j[i].blk_q : J.j[i].blk_amax)) k = i;
+    return k;
+}
+
+// block = (job, 64-column tile, 256-row chunk): column amax, merged with atomicMax on the bit pattern
+// (non-negative floats order like their bits: the result is exact and order-independent)
+__global__ __launch_bounds__(256) void wq_amax_kernel(WqJobs J) {
+    __shared__ float red[4][64];
+    const int ji = find_job(J, blockIdx.x, false);
+    const WqJob& jb = J.j[ji];
+    const int local = blockIdx.x - jb.blk_amax;
+    const int nt = jb.N / 64, kc = local / nt, n0 = (local % nt) * 64;
+    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int k0 = kc * 256, k1 = min(jb.K, k0 + 256);
+    float m = 0.f;
+    for (int k = k0 + rg; k < k1; k += 4) m = fmaxf(m, fabsf(jb.W[(size_t)k * jb.ldw + n0 + col]));
+    red[rg][col] = m;
+    __syncthreads();
+    if (rg == 0) {
+        m = fmaxf(fmaxf(red[0][col], red[1][col]), fmaxf(red[2][col], red[3][col]));
+        atomicMax(jb.amax + n0 + col, __float_as_uint(m));
+    }
+}
+
+// block = (job, 64-column tile, 64-row tile): quantise with the column scale, transpose through LDS,
+// write 64 rows of Wt (one per column) x 64 bytes
+__global__ __launch_bounds__(256) void wq_quant_kernel(WqJobs J) {
+    constexpr int LD = 80;  // bytes per LDS row (16-B aligned reads)
+    __shared__ __attribute__((aligned(16))) uint8_t tile[64 * LD];
+    const int ji = find_job(J, blockIdx.x, true);
+    const WqJob& jb = J.j[ji];
+    const int local = blockIdx.x - jb.blk_q;
+    const int nt = jb.N / 64, kt = local / nt, n0 = (local % nt) * 64, k0 = kt * 64;
+    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const float amax = __uint_as_float(jb.amax[n0 + col]);
+    const float s = amax > 0.f ? amax / 448.f : 1.f;
+    if (kt == 0 && rg == 0) jb.scale[n0 + col] = s;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int kk = rg * 16 + i, k = k0 + kk;
+        const float w = k < jb.K ? jb.W[(size_t)k * jb.ldw + n0 + col] : 0.f;
+        tile[col * LD + kk] = fp8x1(w / s);
+    }
+    __syncthreads();
+    const int n = threadIdx.x >> 2, q = threadIdx.x & 3;
+    if (k0 + q * 16 < jb.K)
+        *reinterpret_cast<uint4*>(jb.Wt + (size_t)(n0 + n) * jb.ldt + k0 + q * 16) =
+            *reinterpret_cast<const uint4*>(tile + n * LD + q * 16);
+}
+
+int quant_weights_fp8(const WqJobs& J0, hipStream_t s) {
+    WqJobs J = J0;
+    ERGM_CHECK_ARG(J.n >= 1 && J.n <= 8, "quant_weights_fp8: 1..8 matrices per launch");
+    int ba = 0, bq = 0;
+    for (int i = 0; i < J.n; ++i) {
+        WqJob& j = J.j[i];
+        ERGM_CHECK_ARG(j.W && j.Wt && j.scale && j.amax && j.N % 64 == 0 && j.K % 64 == 0 && j.ldt >= j.K &&
+                           j.ldt % 16 == 0 && j.ldw >= j.N,
+                       "quant_weights_fp8: bad matrix %d (K=%d N=%d)", i, j.K, j.N);
+        j.blk_amax = ba;
+        j.blk_q = bq;
+        ba += (j.N / 64) * cdiv(j.K, 256);
+        bq += (j.N / 64) * (j.K / 64);
+    }
+    hipLaunchKernelGGL(wq_amax_kernel, dim3(ba), dim3(256), 0, s, J);
+    hipLaunchKernelGGL(wq_quant_kernel, dim3(bq), dim3(256), 0, s, J);
+    return check_launch("quant_weights_fp8");
+}
+
+int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
+                   hipStream_t s) {
+    ERGM_CHECK_ARG(X && Q && scale && rows > 0 && cols > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldx >= cols &&
+                       ldq >= cols && ldq % 8 == 0,
+                   "quant_rows_fp8: bad argument");
+    ERGM_CHECK_ARG(x_dtype == ERGM_BF16 || x_dtype == ERGM_F32, "quant_rows_fp8: bad dtype");
+    dim3 grid(cdiv(rows, 4));
+    auto* q = reinterpret_cast<uint8_t*>(Q);
+    if (x_dtype == ERGM_BF16) hipLaunchKernelGGL(quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+    else hipLaunchKernelGGL(quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+    return check_launch("quant_rows_fp8");
+}
+
+}  // namespace ergm
+
+using namespace ergm;
+
+extern "C" int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq,
+                                   float* scale, void* stream) {
+    return quant_rows_fp8(X, x_dtype, ldx, rows, cols, Q, ldq, scale, as_stream(stream));
+}
+
+extern "C" int ergm_quant_weight_fp8(const float* W, int ldw, int K, int N, void* Wt, int ldt, float* scale,
+                                     void* amax_ws, void* stream) {
+    ERGM_CHECK_ARG(amax_ws, "quant_weight_fp8: amax workspace (N x 4 bytes) required");
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(amax_ws, 0, (size_t)N * 4, s) != hipSuccess) return fail(ERGM_EHIP, "quant_weight_fp8: memset");
+    WqJobs J{};
+    J.n = 1;
+    J.j[0] = WqJob{W, reinterpret_cast<uint8_t*>(Wt), scale, reinterpret_cast<unsigned*>(amax_ws), ldw, K, N, ldt, 0, 0};
+    return quant_weights_fp8(J, s);
+}

@@ -52,6 +52,49 @@ def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int
     return out
 
 
+def gemm_f8(A8: torch.Tensor, a_scale: torch.Tensor, B8t: torch.Tensor, b_scale: torch.Tensor,
+            out: Optional[torch.Tensor] = None, out_dtype=torch.float32, epilogue: int = L.EPI_NONE,
+            bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+            aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0) -> torch.Tensor:
+    """C[M,N] = epilogue(alpha · a_scale[m] · b_scale[n] · A8[m]·B8t[n]); A8 [M,K], B8t [N,K] e4m3 bytes
+    (uint8 or torch.float8_e4m3fn), a_scale [M], b_scale [N] f32."""
+    _need_gpu(A8, B8t, a_scale, b_scale)
+    M, K = A8.shape
+    N = B8t.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=A8.device)
+    d = L.GemmDesc(M=M, N=N, K=K, lda=A8.stride(0), ldb=B8t.stride(0), ldc=out.stride(0), a_layout=L.MK,
+                   b_layout=L.NK, c_dtype=L.BF16 if out.dtype == torch.bfloat16 else L.F32, epilogue=epilogue,
+                   alpha=alpha, bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
+                   aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0)
+    L.check(L.load().ergm_gemm_f8(C.byref(d), _ptr(A8), _ptr(a_scale), _ptr(B8t), _ptr(b_scale), _ptr(out),
+                                  _stream(A8.device)), "ergm_gemm_f8")
+    return out
+
+
+def quant_rows_fp8(X: torch.Tensor, cols: Optional[int] = None):
+    """Row-wise e4m3 quantisation: returns (Q [rows, cols] uint8, scale [rows] f32)."""
+    _need_gpu(X)
+    rows = X.shape[0]
+    cols = X.shape[1] if cols is None else cols
+    Q = torch.empty(rows, cols, dtype=torch.uint8, device=X.device)
+    sc = torch.empty(rows, dtype=torch.float32, device=X.device)
+    dt = L.BF16 if X.dtype == torch.bfloat16 else L.F32
+    L.call("ergm_quant_rows_fp8", _ptr(X), dt, X.stride(0), rows, cols, _ptr(Q), cols, _ptr(sc), _stream(X.device))
+    return Q, sc
+
+
+def quant_weight_fp8(W: torch.Tensor):
+    """Conv1D weight W f32 [K, N] → (Wt [N, K] e4m3 bytes, scale [N] f32), column-wise scales."""
+    _need_gpu(W)
+    K, N = W.shape
+    Wt = torch.empty(N, K, dtype=torch.uint8, device=W.device)
+    sc = torch.empty(N, dtype=torch.float32, device=W.device)
+    ws = torch.empty(N, dtype=torch.int32, device=W.device)
+    L.call("ergm_quant_weight_fp8", _ptr(W), W.stride(0), K, N, _ptr(Wt), K, _ptr(sc), _ptr(ws), _stream(W.device))
+    return Wt, sc
+
+
 def attn_fwd(q, k, v, B, H, Sq, Sk, causal, o=None, lse=None):
     """q/k/v: 2-D token-major views [B*S, ld] whose first column is head 0, dim 0."""
     _need_gpu(q, k, v)

@@ -35,7 +35,8 @@ class ModelRunner:
         self.dims = L.ModelDims(vocab=layout.vocab, vocab_pad=layout.vocab_pad, n_embd=E, n_layer=Lyr,
                                 n_head=cfg.n_head, n_inner=layout.F, n_positions=layout.P, batch=B, seq=S,
                                 eps=cfg.layer_norm_epsilon, has_features=int(has_features),
-                                ld_vis=vis_rows * layout.Fd if has_features else 0, feat_dim=layout.Fd)
+                                ld_vis=vis_rows * layout.Fd if has_features else 0, feat_dim=layout.Fd,
+                                fp8=int(bool(getattr(cfg, "fp8", False))))
         ws_bytes = self.lib.ergm_model_workspace_size(C.byref(self.dims))
         self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=self.dev)
         v = layout.views
@@ -56,6 +57,7 @@ class ModelRunner:
         prm.ln_f_w, prm.ln_f_b = f32("transformer.ln_f.weight"), f32("transformer.ln_f.bias")
         prm.emo_w = f32("emotion_head.weight")
         prm.capkv_w_b, prm.capkv_b = b16("__capkv_w"), f32("__capkv_b")
+        prm.capkv_w = f32("__capkv_w")
         prm.layer_f32 = C.c_void_p(fp + 4 * layout.layer_base[0])
         prm.layer_b16 = C.c_void_p(bp + 2 * layout.layer_base[0])
         prm.layer_stride = layout.layer_stride

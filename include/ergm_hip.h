@@ -97,6 +97,25 @@ size_t ergm_gemm_workspace_size(const ergm_gemm_desc* desc);
 int ergm_gemm(const ergm_gemm_desc* desc, const void* A, const void* B, void* C, void* workspace,
               size_t ws_bytes, void* stream);
 
+/* fp8 GEMM (config 5's forward Conv1D GEMMs; build-side, the reference is fp32):
+ *   C = epilogue(alpha · a_scale[m] · b_scale[n] · Σ_k A[m][k]·B[n][k])
+ * A [M][lda], B [N][ldb]: OCP e4m3fn bytes, k contiguous (desc->a_layout = ERGM_MK, b_layout =
+ * ERGM_NK); K % 128 == 0; lda, ldb multiples of 16.  Runs v_mfma_scale_f32_16x16x128_f8f6f4 (unit
+ * block scales; 2x the bf16 MFMA rate).  Epilogues: NONE (f32/bf16 C), BIAS / BIAS_GELU (bf16 C),
+ * BIAS_RESID (f32 C).  ergm_gemm_f8_tune forces a tile configuration (-1 = automatic).           */
+int ergm_gemm_f8(const ergm_gemm_desc* desc, const void* A, const float* a_scale, const void* B,
+                 const float* b_scale, void* C, void* stream);
+int ergm_gemm_f8_tune(int cfg);
+/* Row-wise e4m3 quantisation (activations): scale[r] = max_c |X[r][c]| / 448 (1 for a zero row),
+ * Q[r][c] = e4m3(clamp(X[r][c] / scale[r], ±448)).  X bf16 or f32 (x_dtype), cols % 8 == 0.       */
+int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq,
+                        float* scale, void* stream);
+/* Column-wise e4m3 quantisation of a Conv1D weight W f32 [K][ldw] (in, out) into its transpose
+ * Wt [N][ldt] (k contiguous, the B operand of ergm_gemm_f8): scale[n] = max_k |W[k][n]| / 448.
+ * amax_ws: N x 4 bytes of workspace.  K, N multiples of 64.                                      */
+int ergm_quant_weight_fp8(const float* W, int ldw, int K, int N, void* Wt, int ldt, float* scale,
+                          void* amax_ws, void* stream);
+
 /* Fused attention over head_dim = 64, token-major tensors with head h at columns [64h, 64h+64):
  *   Q[b][s][h*64+d] = q + (b*Sq + s)*ldq + h*64 + d     (likewise K/V with Sk rows, O with ldo)
  * out: O (bf16) and lse[b][h][s] = ln Σ_k exp(score) (f32; backward recomputes P from it).
@@ -202,6 +221,10 @@ typedef struct {
     int feat_dim;             /* Fd: width of the pooled features; 0 or n_embd = added directly
                                * (src/model.py:497-498); otherwise a Conv1D projection per modality
                                * (build-side, config 5: 768-d features into a 1024-d backbone) */
+    int fp8;                  /* 1: the forward Conv1D GEMMs of every block (and the caption K/V
+                               * GEMM) run on ergm_gemm_f8 with per-row activation / per-column
+                               * weight scales; weights are re-quantised from the f32 master at
+                               * every forward; LM head, backward and optimizer stay bf16/f32 */
 } ergm_model_dims;
 
 /* Pointer table: names follow the reference state_dict; see ergm_amd/model.py. */
@@ -224,6 +247,8 @@ typedef struct {
      * shadow), biases [E] f32, gradients f32; each bias stored right after its weight */
     const void* vproj_w_b; const float* vproj_b; const void* aproj_w_b; const float* aproj_b;
     float* g_vproj_w; float* g_vproj_b; float* g_aproj_w; float* g_aproj_b;
+    /* fp32 master of the stacked caption K/V weight [E][L*2E] (read by the fp8 weight quantiser) */
+    const float* capkv_w;
 } ergm_model_params;
 
 typedef enum {
