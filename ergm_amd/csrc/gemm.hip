@@ -12,6 +12,7 @@
 // m/n-contiguous tiles are read column-wise with ds_read_b64_tr_b16 (CDNA4 transpose read) under a
 // row-dependent chunk XOR that keeps each 32-lane half conflict-free.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -753,13 +754,20 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
         // weight gradients (A = activations^T), deep K split 4 ways, 64x64 without split otherwise
         // (split-K's extra reduce launch cost more than it saved at these sizes).
         const long t128 = tiles_of(M, N, 128, 128);
-        if (K >= 4096 && t128 < 240 && d->split_k != 1) {
+        const bool km = d->a_layout == ERGM_KM;
+        if (K >= 32768 && t128 < 240 && d->split_k != 1) {
+            // contraction over the vocabulary (LM-head dX) / the stacked caption K/V at config 5: the
+            // 256x256 tile, split until ~256 workgroups (tools/gemm_tune.py: c6s8 at C2, c6s4 at C5)
+            p.cfg = 6;
+            split = (int)std::max(1L, std::min(8L, 256 / std::max(1L, tiles_of(M, N, 256, 256))));
+        } else if (K >= 4096 && t128 < 240 && d->split_k != 1) {
             p.cfg = 2;
-            split = std::max(1, std::min(4, K / 1024));
+            // weight gradients over T >= 4096 tokens (config 5): split only the smallest outputs
+            split = km ? (t128 < 100 ? 3 : 1) : std::max(1, std::min(4, K / 1024));
         } else if (t128 >= 4000) {
             p.cfg = 6;
         } else if (t128 >= 140) {
-            p.cfg = d->a_layout == ERGM_KM ? 2 : 10;
+            p.cfg = km ? 2 : (K >= 3072 ? 14 : 10);
         } else {
             p.cfg = 0;
         }

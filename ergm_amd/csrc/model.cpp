@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -98,6 +99,11 @@ struct ergm_model_plan {
     float *capkv8_s, *sa, *sf, *scap;
     unsigned* capkv_amax;
     std::vector<hipEvent_t> ev_wq;
+    // forward batch-half chains: the second runs on fwd2 (ev_f2: fork, embedding done, chain done)
+    int fwd_chains;
+    hipStream_t fwd2;
+    hipEvent_t ev_f2[3];
+    char* scratch3;
     // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
@@ -266,7 +272,7 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
-    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : P->scratch;
+    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : (s != nullptr && s == P->fwd2) ? P->scratch3 : P->scratch;
     return ergm_gemm(&g, A, B, C, ws, P->scratch_bytes, s);
 }
 
@@ -286,7 +292,7 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
 int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, int cols, int ldx, float* out) {
     ERGM_TRY(ws_need(P, ergm_colsum_workspace_size(rows, cols)));
     if (P->dry) return ERGM_OK;
-    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : P->scratch;
+    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : (s != nullptr && s == P->fwd2) ? P->scratch3 : P->scratch;
     return ergm_colsum(X, dt, rows, cols, ldx, out, 0, ws, P->scratch_bytes, s);
 }
 
@@ -412,11 +418,15 @@ extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     P.need = ergm_embed_bwd_workspace_size(P.T);
     P.need = std::max(P.need, ergm_colsum_workspace_size(P.T, std::max(P.L2E, dims->n_inner)));
     P.labels = P.emo_labels = nullptr;
-    do_forward(&P, nullptr, nullptr, nullptr, 1, nullptr);
+    P.fwd2 = nullptr;
+    for (int chains = 1; chains <= 2; ++chains) {  // size for the whole batch and for its halves
+        P.fwd_chains = chains;
+        do_forward(&P, nullptr, nullptr, nullptr, 1, nullptr);
+    }
     do_backward_head(&P, nullptr, nullptr);
     do_backward_layer(&P, 0, nullptr);
     do_backward_embed(&P, nullptr);
-    return ((act + 255) & ~(size_t)255) + 2 * (((P.need + 255) & ~(size_t)255) + 256);
+    return ((act + 255) & ~(size_t)255) + 3 * (((P.need + 255) & ~(size_t)255) + 256);
 }
 
 extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* ws,
@@ -452,15 +462,23 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->L2E = 2 * d.n_embd * d.n_layer;
     size_t act = carve(P, reinterpret_cast<char*>(ws));
     act = (act + 255) & ~(size_t)255;
-    P->scratch_bytes = (ws_bytes - act) / 2 & ~(size_t)255;
+    P->scratch_bytes = (ws_bytes - act) / 3 & ~(size_t)255;
     P->scratch = reinterpret_cast<char*>(ws) + act;
     P->scratch2 = P->scratch + P->scratch_bytes;
+    P->scratch3 = P->scratch2 + P->scratch_bytes;
     P->side = nullptr;
     P->ev_fork = nullptr;
     P->ev_join.assign(d.n_layer + 3, nullptr);
     bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
+    // ERGM_FWD_CHAINS=1 disables the two-chain forward (A/B measurements)
+    P->fwd_chains = 2;
+    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = atoi(e);
+    P->fwd2 = nullptr;
+    for (auto& e : P->ev_f2) e = nullptr;
+    ok = ok && hipStreamCreateWithFlags(&P->fwd2, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : P->ev_f2) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     P->ev_wq.assign(P->f8 ? d.n_layer : 0, nullptr);
     for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
@@ -516,6 +534,12 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
         if (e) hipEventDestroy(e);
     for (auto e : P->ev_wq)
         if (e) hipEventDestroy(e);
+    for (auto e : P->ev_f2)
+        if (e) hipEventDestroy(e);
+    if (P->fwd2) {
+        hipStreamSynchronize(P->fwd2);
+        hipStreamDestroy(P->fwd2);
+    }
     if (P->ev_fork) hipEventDestroy(P->ev_fork);
     if (P->side) hipStreamDestroy(P->side);
     delete P;
@@ -561,9 +585,104 @@ extern "C" int ergm_model_set_inputs(ergm_model_plan* P, const int64_t* ids, con
 }
 
 namespace {
+// One block's forward (src/model.py:286-341) over the batch rows [b0, b0+nb) on stream s: every
+// kernel is row- (or batch-) separable, so two such chains over disjoint halves of the batch run
+// concurrently on two streams and write disjoint rows of the same activation buffers — the backward
+// sees the full-batch layout unchanged.
+int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
+    const ergm_model_dims& d = P->d;
+    const int E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, S = d.seq, L2E = P->L2E;
+    const int T = nb * S;
+    const size_t r0 = (size_t)b0 * S, XE = P->XE, XF = P->XF;
+    const LayerActs& a0 = P->la[l];
+    LayerActs a = a0;
+    if (!P->dry) {
+        a.ln1 += r0 * XE; a.lnx += r0 * XE; a.ln2 += r0 * XE;
+        a.m1 += r0; a.r1 += r0; a.mx += r0; a.rx += r0; a.m2 += r0; a.r2 += r0;
+        a.qkv += r0 * 3 * E; a.ao += r0 * XE; a.xq += r0 * E; a.xo += r0 * XE;
+        a.pre += r0 * F; a.act += r0 * XF;
+        a.lse += (size_t)b0 * H * S; a.xlse += (size_t)b0 * H * S;
+    }
+    float* x0 = P->dry ? nullptr : P->resid[3 * l] + r0 * E;
+    float* x1 = P->dry ? nullptr : P->resid[3 * l + 1] + r0 * E;
+    float* x2 = P->dry ? nullptr : P->resid[3 * l + 2] + r0 * E;
+    float* x3 = P->dry ? nullptr : P->resid[3 * l + 3] + r0 * E;
+    // fp8 (config 5): every Conv1D below consumes row-quantised activations (the LayerNorms write
+    // their fp8 copy themselves, attention / GELU outputs go through quant_rows_fp8) and block l's
+    // re-quantised weights, which the side stream marks ready with ev_wq[l]
+    const bool f8 = P->f8;
+    const LayerW8* w8 = f8 && !P->dry ? &P->w8[l] : nullptr;
+    uint8_t* qa = f8 && !P->dry ? P->qa + r0 * E : nullptr;
+    uint8_t* qf = f8 && !P->dry ? P->qf + r0 * F : nullptr;
+    float* sa = f8 && !P->dry ? P->sa + r0 : nullptr;
+    float* sf = f8 && !P->dry ? P->sf + r0 : nullptr;
+    if (w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
+    // self-attention sub-block (src/model.py:297-309)
+    if (!P->dry)
+        ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
+                                  d.eps, s, qa, E, sa));
+    if (f8)
+        ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
+                       ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+    else
+        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
+                      ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+    if (!P->dry)
+        ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, nb, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
+                               s));
+    if (f8) {
+        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
+        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+    } else {
+        ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+    }
+    // cross-attention over caption embeddings (src/model.py:311-329)
+    if (!P->dry)
+        ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
+                                  d.eps, s, qa, E, sa));
+    if (f8)
+        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E, ERGM_BF16,
+                       ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+    else
+        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
+                      ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+    const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
+    if (l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
+    if (!P->dry)
+        ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, s));
+    if (f8) {
+        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
+        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+    } else {
+        ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+    }
+    // MLP (src/model.py:331-334, 262-267)
+    if (!P->dry)
+        ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
+                                  d.eps, s, qa, E, sa));
+    if (f8) {
+        ERGM_TRY(gemm8(P, s, T, F, E, qa, sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
+                       ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
+        ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E, ERGM_F32,
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+    } else {
+        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF, ERGM_BF16,
+                      ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+        ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+    }
+    (void)L;
+    return ERGM_OK;
+}
+
 int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s) {
     const ergm_model_dims& d = P->d;
-    const int T = P->T, E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, B = d.batch, S = d.seq;
+    const int T = P->T, E = d.n_embd, L = d.n_layer, B = d.batch, S = d.seq;
     const int L2E = P->L2E;
     const ergm_model_params& p = P->p;
 
@@ -583,14 +702,35 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         aud_in = P->proj_out ? P->proj_out + (size_t)Bp * E : nullptr;
         ld_vis = E;
     }
-    if (!P->dry)
-        ERGM_TRY(embed_fwd_ld(P->ids, P->tt, P->cap_ids, p.wte, p.wpe, vis_in, ld_vis, aud_in, P->resid[0], P->cap,
-                              P->XE, B, S, E, d.vocab, s));
+    // Two concurrent chains over the two halves of the batch (main stream: rows of batch [0, B0);
+    // P->fwd2: [B0, B)): the forward is a serial chain of mostly latency-bound kernels, and a second
+    // independent chain fills the CUs the first leaves idle.  nchain = 1 when B = 1 (or disabled).
+    const int nchain = (B >= 2 && P->fwd_chains >= 2) ? 2 : 1;
+    const int bsplit[3] = {0, nchain == 2 ? B / 2 : B, B};
+    hipStream_t cs[2] = {s, P->dry ? s : P->fwd2};
+    auto embed = [&](int c) -> int {
+        if (P->dry) return ERGM_OK;
+        const int b0 = bsplit[c], nb = bsplit[c + 1] - b0;
+        const size_t r0 = (size_t)b0 * S;
+        return embed_fwd_ld(P->ids + r0, P->tt ? P->tt + r0 : nullptr, P->cap_ids + r0, p.wte, p.wpe,
+                            vis_in ? vis_in + (size_t)b0 * ld_vis : nullptr, ld_vis,
+                            aud_in ? aud_in + (size_t)b0 * E : nullptr, P->resid[0] + r0 * E, P->cap + r0 * P->XE,
+                            P->XE, nb, S, E, d.vocab, cs[c]);
+    };
+    if (nchain == 2 && !P->dry) {
+        if (hipEventRecord(P->ev_f2[0], s) != hipSuccess || hipStreamWaitEvent(P->fwd2, P->ev_f2[0], 0) != hipSuccess)
+            return fail(ERGM_EHIP, "model: chain fork");
+        ERGM_TRY(embed(1));
+        if (hipEventRecord(P->ev_f2[1], P->fwd2) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+    }
+    ERGM_TRY(embed(0));
     // all L cross-attention K/V projections of the caption embeddings in one GEMM, on the side stream
     // (it overlaps block 0's self-attention; joined before block 0's cross-attention)
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
+        if (nchain == 2 && !P->dry && hipStreamWaitEvent(ss, P->ev_f2[1], 0) != hipSuccess)
+            return fail(ERGM_EHIP, "model: stream wait");
         if (P->f8) ERGM_TRY(quant_layer_weights(P, 0, ss));
         // the embedding backward's sort needs only the ids: done here, off the critical chain
         if (train && !P->dry)
@@ -616,78 +756,11 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         if (P->f8)
             for (int l = 1; l < L; ++l) ERGM_TRY(quant_layer_weights(P, l, ss));
     }
-    for (int l = 0; l < L; ++l) {
-        LayerActs& a = P->la[l];
-        float* x0 = P->resid[3 * l];
-        float* x1 = P->resid[3 * l + 1];
-        float* x2 = P->resid[3 * l + 2];
-        float* x3 = P->resid[3 * l + 3];
-        // fp8 (config 5): every Conv1D below consumes row-quantised activations (the LayerNorms write
-        // their fp8 copy themselves, attention / GELU outputs go through quant_rows_fp8) and block l's
-        // re-quantised weights, which the side stream marks ready with ev_wq[l]
-        const bool f8 = P->f8;
-        const LayerW8* w8 = f8 && !P->dry ? &P->w8[l] : nullptr;
-        uint8_t* qa = f8 ? P->qa : nullptr;
-        if (w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
-        // self-attention sub-block (src/model.py:297-309)
-        if (!P->dry)
-            ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
-                                      d.eps, s, qa, E, P->sa));
-        if (f8)
-            ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, P->sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
-                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
-        else
-            ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
-                          ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
-        if (!P->dry)
-            ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
-                                   s));
-        if (f8) {
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, P->sa, s));
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
-                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
-        } else {
-            ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
-                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
-        }
-        // cross-attention over caption embeddings (src/model.py:311-329)
-        if (!P->dry)
-            ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
-                                      d.eps, s, qa, E, P->sa));
-        if (f8)
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E,
-                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
-        else
-            ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
-                          ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
-        const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
-        if (l == 0) ERGM_TRY(join_side(P, s, L));
-        if (!P->dry)
-            ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, B, H, S, S, E, L2E, L2E, P->XE, 0, s));
-        if (f8) {
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, P->sa, s));
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, P->sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
-                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
-        } else {
-            ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
-                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
-        }
-        // MLP (src/model.py:331-334, 262-267)
-        if (!P->dry)
-            ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
-                                      d.eps, s, qa, E, P->sa));
-        if (f8) {
-            ERGM_TRY(gemm8(P, s, T, F, E, qa, P->sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
-                           ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, P->qf, F, P->sf, s));
-            ERGM_TRY(gemm8(P, s, T, E, F, P->qf, P->sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E,
-                           ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
-        } else {
-            ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF,
-                          ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-            ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
-                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
-        }
+    for (int l = 0; l < L; ++l)  // enqueue block by block, alternating chains
+        for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
+    if (nchain == 2 && !P->dry) {
+        if (hipEventRecord(P->ev_f2[2], P->fwd2) != hipSuccess || hipStreamWaitEvent(s, P->ev_f2[2], 0) != hipSuccess)
+            return fail(ERGM_EHIP, "model: chain join");
     }
     if (!P->dry)
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));

@@ -198,19 +198,22 @@ struct LnReduceJobs {  // up to 4 LayerNorms' (partials, dγ, dβ) reduced by on
     float* dbeta[4];
 };
 
-__global__ __launch_bounds__(1024) void ln_param_reduce_kernel(LnReduceJobs jobs, int nparts, int E) {
-    __shared__ float red[16][64];
+// 256-thread blocks (32 columns x 8 row lanes, 16 partial rows in flight per lane): small enough to
+// find free wave slots beside the GEMMs running concurrently on the other streams (a 1024-thread
+// block needs a whole CU's slots and waited behind long GEMM tiles at config-5 sizes).
+__global__ __launch_bounds__(256) void ln_param_reduce_kernel(LnReduceJobs jobs, int nparts, int E) {
+    __shared__ float red[8][32];
     const int z = blockIdx.z;
     const float* part = blockIdx.y == 0 ? jobs.part_g[z] : jobs.part_b[z];
     float* out = blockIdx.y == 0 ? jobs.dgamma[z] : jobs.dbeta[z];
-    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
+    const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+    const int c = blockIdx.x * 32 + cl;
     float acc = 0.f;
-    for (int base = 0; base < nparts; base += 256) {
+    for (int base = 0; base < nparts; base += 128) {
         float v[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const int r = base + rl + 16 * j;
+            const int r = base + rl + 8 * j;
             v[j] = c < E && r < nparts ? part[(size_t)r * E + c] : 0.f;
         }
 #pragma unroll
@@ -222,13 +225,13 @@ __global__ __launch_bounds__(1024) void ln_param_reduce_kernel(LnReduceJobs jobs
     red[rl][cl] = acc;
     __syncthreads();
     if (rl == 0 && c < E) {
-        float t[16];
+        float t[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) t[j] = red[j][cl];
+        for (int j = 0; j < 8; ++j) t[j] = red[j][cl];
 #pragma unroll
-        for (int w = 1; w < 16; w <<= 1)
+        for (int w = 1; w < 8; w <<= 1)
 #pragma unroll
-            for (int j = 0; j < 16; j += 2 * w) t[j] += t[j + w];
+            for (int j = 0; j < 8; j += 2 * w) t[j] += t[j + w];
         out[c] = t[0];
     }
 }
@@ -396,7 +399,7 @@ int layernorm_param_reduce_n(int n, const float* const* part_g, const float* con
         ERGM_CHECK_ARG(part_g[i] && part_b[i] && dgamma[i] && dbeta[i], "layernorm_param_reduce: null argument");
         j.part_g[i] = part_g[i]; j.part_b[i] = part_b[i]; j.dgamma[i] = dgamma[i]; j.dbeta[i] = dbeta[i];
     }
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 64), 2, n), dim3(1024), 0, s, j, ln_bwd_nparts(rows), E);
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 32), 2, n), dim3(256), 0, s, j, ln_bwd_nparts(rows), E);
     return check_launch("layernorm_param_reduce");
 }
 

@@ -2,7 +2,7 @@
 
 Each (shape, config, split) is captured 20x into a HIP graph (torch.cuda.CUDAGraph) and replayed, so
 host launch overhead is excluded; prints a table and the best config per shape, and writes
-gpurun_out/gemm_tune.json.  Usage (on the GPU box):  python tools/gemm_tune.py [--quick]
+gpurun_out/gemm_tune.json.  Usage (on the GPU box):  python tools/gemm_tune.py [--quick] [--c5]
 """
 import ctypes as C
 import json
@@ -15,6 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ergm_amd import _lib as L  # noqa: E402
 
 T, E, F, LYR, VP = 2048, 768, 3072, 12, 50304
+if "--c5" in sys.argv:  # config 5 geometry (GPT-2-medium, B=32, S=128); its forward GEMMs run fp8
+    T, E, F, LYR = 4096, 1024, 4096, 24
 L2E = 2 * E * LYR
 MK, KM, NK, KN = L.MK, L.KM, L.NK, L.KN
 BF, FP = L.BF16, L.F32
@@ -87,7 +89,10 @@ def main():
     results = []
     total_best = 0.0
     total_auto = 0.0
+    only_bwd = "--c5" in sys.argv
     for (name, cnt, M, N, K, al, lda, bl, ldb, epi, cdt) in SHAPES:
+        if only_bwd and name.startswith("fwd") and name != "fwd lm_head":
+            continue
         a_rows = M if al == MK else K
         b_rows = N if bl == NK else K
         A = (torch.randn(a_rows, lda, generator=g) * 0.1).bfloat16().to(dev)

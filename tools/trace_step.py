@@ -1,12 +1,12 @@
 """Per-step breakdown of a rocprofv3 kernel trace of bench.py: the last complete training step
-(embedding forward of step i .. embedding forward of step i+1), busy time per stream, idle gaps and
+(embedding sort of step i .. embedding sort of step i+1), busy time per stream, idle gaps and
 the top kernels.  Usage: python tools/trace_step.py <rocprof output dir> [top-N]"""
 import csv, sys
 from collections import defaultdict
 d = sys.argv[1]
 rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-st = [i for i, r in enumerate(rows) if 'embed_fwd' in r['Kernel_Name']]
+st = [i for i, r in enumerate(rows) if 'embed_sort' in r['Kernel_Name']]
 a, b = st[-2], st[-1]
 step = rows[a:b]
 t0 = int(step[0]['Start_Timestamp']); t1 = max(int(r['End_Timestamp']) for r in step)
