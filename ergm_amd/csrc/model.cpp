@@ -99,6 +99,10 @@ struct ergm_model_plan {
     float *capkv8_s, *sa, *sf, *scap;
     unsigned* capkv_amax;
     std::vector<hipEvent_t> ev_wq;
+    // per_stage_join: the caller's stream waits for block l+1's side-stream weight gradients at the end
+    // of stage l (ergm_model_backward_layer's ordering guarantee); 0 = only the embedding stage joins,
+    // consumers of a block's gradients wait with ergm_model_stage_wait instead
+    bool per_stage_join;
     // forward batch-half chains: the second runs on fwd2 (ev_f2: fork, embedding done, chain done)
     int fwd_chains;
     hipStream_t fwd2;
@@ -475,6 +479,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     // ERGM_FWD_CHAINS=1 disables the two-chain forward (A/B measurements)
     P->fwd_chains = 2;
     if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = atoi(e);
+    P->per_stage_join = true;
     P->fwd2 = nullptr;
     for (auto& e : P->ev_f2) e = nullptr;
     ok = ok && hipStreamCreateWithFlags(&P->fwd2, hipStreamNonBlocking) == hipSuccess;
@@ -553,6 +558,20 @@ extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begi
     P->ev_begin = reinterpret_cast<hipEvent_t>(ev_begin);
     P->ev_end = reinterpret_cast<hipEvent_t>(ev_end);
     return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_side_joins(ergm_model_plan* P, int per_stage) {
+    ERGM_CHECK_ARG(P, "model_set_side_joins: null plan");
+    P->per_stage_join = per_stage != 0;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_stage_wait(ergm_model_plan* P, int stage, void* stream) {
+    ERGM_CHECK_ARG(P && stage >= 0 && stage < P->d.n_layer + 3 && stage != P->d.n_layer,
+                   "model_stage_wait: stage in [0, L) or L+1, L+2");
+    return hipStreamWaitEvent(as_stream(stream), P->ev_join[stage], 0) == hipSuccess
+               ? ERGM_OK
+               : fail(ERGM_EHIP, "model_stage_wait: hipStreamWaitEvent");
 }
 
 extern "C" int ergm_model_set_row_flags(ergm_model_plan* P, void* row_flag, int n) {
@@ -889,7 +908,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // those of the block differentiated before, so block l+1's gradients are final on return.
     ERGM_TRY(ln_reduce_flush(P, s));  // this block's three LayerNorms (+ ln_f after the head stage)
     ERGM_TRY(side_mark(P, l));
-    if (l + 1 < L) ERGM_TRY(join_side(P, s, l + 1));
+    if (l + 1 < L && P->per_stage_join) ERGM_TRY(join_side(P, s, l + 1));
     return ERGM_OK;
 }
 

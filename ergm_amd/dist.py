@@ -58,9 +58,11 @@ class DPSync:
             self._stream = torch.cuda.Stream(dev)
         return self._stream
 
-    def enqueue(self, grad: torch.Tensor, fn, key: int) -> None:
+    def enqueue(self, grad: torch.Tensor, fn, key: int, wait=None) -> None:
         """Run ``fn()`` on the side stream once everything issued so far on the current stream is
-        done (``key`` selects the reusable ordering event; fn launches work, it does not wait)."""
+        done (``key`` selects the reusable ordering event; fn launches work, it does not wait).
+        ``wait(stream_handle)``, if given, adds a further dependency of the side stream (the executor's
+        weight-gradient stream mark of the bucket, ergm_model_stage_wait)."""
         if not grad.is_cuda:
             fn()
             return
@@ -72,10 +74,12 @@ class DPSync:
         ev = self._events[key]  # reused every step: the wait below is enqueued right after the record
         ev.record(cur.cuda_stream)
         ev.wait(side.cuda_stream)
+        if wait is not None:
+            wait(side.cuda_stream)
         with torch.cuda.stream(side):
             fn()
 
-    def bucket_ready(self, k: int, grad: torch.Tensor, post=None) -> None:
+    def bucket_ready(self, k: int, grad: torch.Tensor, post=None, wait=None) -> None:
         """Bucket k of the flat gradient buffer `grad` is final on the current stream: start its
         all-reduce (SUM) on the side stream, then run ``post(a, b)`` there once the reduced values are
         in place (the overlapped optimizer update of that parameter range)."""
@@ -93,7 +97,7 @@ class DPSync:
                     self._works.append(work)
             if post is not None:
                 post(a, b)
-        self.enqueue(grad, run, k)
+        self.enqueue(grad, run, k, wait)
 
     def finish(self, grad: torch.Tensor) -> None:
         """Make the current stream wait for every outstanding bucket (no host synchronisation)."""

@@ -78,6 +78,12 @@ class ModelRunner:
         L.check(self.lib.ergm_model_create(C.byref(self.dims), C.byref(prm), _p(self.workspace), ws_bytes,
                                            C.byref(plan)), "ergm_model_create")
         self.plan = plan
+        # the data-gradient chain never waits for the weight-gradient stream between blocks; the
+        # consumers of each block's gradients (all-reduce, overlapped AdamW) wait for its mark instead
+        # (ERGM_SIDE_JOINS=1 restores the per-stage joins, for A/B measurements)
+        import os
+        self.per_stage_join = os.environ.get("ERGM_SIDE_JOINS", "0") == "1"
+        L.check(self.lib.ergm_model_set_side_joins(self.plan, int(self.per_stage_join)), "ergm_model_set_side_joins")
         self.grad = grad
         self.dp = DPSync(process_group, dp_buckets(layout))
         self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)
@@ -218,13 +224,18 @@ class ModelRunner:
                         "ergm_rows_compact")
             if post is not None:
                 post(wa, wb, rows=(E, self.row_flags, 1))
-        # bucket i = (head +) block L-1-i; its weight gradients are joined one stage later (ergm_hip.h)
+        def stage(k):  # the consumer stream also waits for the executor's weight-gradient mark k
+            if self.per_stage_join:
+                return None
+            return lambda st: L.check(lib.ergm_model_stage_wait(self.plan, k, C.c_void_p(st)), "ergm_model_stage_wait")
+        # bucket i = (head +) block L-1-i; its data-gradient chain is done after stage L-1-i, its weight
+        # gradients (side stream) at mark L-1-i; the LM-head part of wte at mark L+1 (ergm_hip.h)
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
             if i >= 1:
-                dp.bucket_ready(i - 1, self.grad, post)
+                dp.bucket_ready(i - 1, self.grad, post, wait=stage(l + 1))
             if split_wte and i == 1:
-                dp.enqueue(self.grad, wte_lm_rows, ka)
+                dp.enqueue(self.grad, wte_lm_rows, ka, wait=stage(Lyr + 1))
         if compact:
             self._ev_zero.wait(s.value)  # compact rows zeroed before the lookup sums land in them
             self._compact_ready = False

@@ -301,6 +301,15 @@ int ergm_model_forward(ergm_model_plan* plan, void* logits, float* emo_logits, f
 int ergm_model_backward_head(ergm_model_plan* plan, const float* grad_scale_dev, void* stream);
 int ergm_model_backward_layer(ergm_model_plan* plan, int layer, void* stream);
 int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
+/* Side-stream joins.  per_stage = 1 (default): the ordering guarantee above.  per_stage = 0: the
+ * caller's stream does not wait for block l+1's weight gradients at the end of stage l (so the
+ * data-gradient chain never idles behind the weight-gradient GEMMs); only backward_embed joins, after
+ * which every gradient is final on `stream` as before.  A consumer of block l's gradients (a DP
+ * all-reduce, an overlapped optimizer) then makes its stream wait with ergm_model_stage_wait(plan, l,
+ * its_stream) after the stage that finalises it was enqueued; stage L+1 = the LM-head (tied wte)
+ * weight gradient, L+2 = the caption K/V / projection weight gradients.                             */
+int ergm_model_set_side_joins(ergm_model_plan* plan, int per_stage);
+int ergm_model_stage_wait(ergm_model_plan* plan, int stage, void* stream);
 
 /* Kernel probe for in-loop timing: while set, the executor records `ev_begin` / `ev_end`
  * (hipEvent_t, passed as void*) on the stream immediately around the probed launch:
