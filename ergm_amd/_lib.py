@@ -63,7 +63,7 @@ _SIGS = {
     "ergm_gemm_f8": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, vp, vp]),
     "ergm_gemm_f8_tune": (i32, [i32]),
     "ergm_quant_rows_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp]),
-    "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp]),
+    "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp]),
     "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "ergm_attn_tune": (i32, [i32]),
     "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),

@@ -47,12 +47,13 @@ __device__ __forceinline__ float bits2f(uint16_t b) { return __uint_as_float(((u
 
 // fp8 weight quantisation jobs (quant.hip), batched over the matrices of one block
 struct WqJob {
-    const float* W;       // [K][ldw] f32 (Conv1D [in, out])
+    const void* W;        // [K][ldw] f32 or bf16 (Conv1D [in, out]), see w_bf16
     uint8_t* Wt;          // [N][ldt] e4m3 (transposed)
     float* scale;         // [N]
     unsigned* amax;       // [N] |w| bit patterns, zeroed by the caller
     int ldw, K, N, ldt;
     int blk_amax, blk_q;  // first block of this job in each grid (set by quant_weights_fp8)
+    int w_bf16;           // W is the bf16 shadow (the executor) rather than the f32 master
 };
 struct WqJobs {
     WqJob j[8];

@@ -382,7 +382,8 @@ inline float* LG(const ergm_model_plan* P, int l, int t) {
     return P->p.g_layer + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
 }
 
-// Re-quantise block l's six Conv1D weights (f32 master → transposed e4m3 + column scales) on `ss` and
+// Re-quantise block l's six Conv1D weights (bf16 shadow → transposed e4m3 + column scales: half the bytes
+// of the f32 master, and the values the bf16 backward GEMMs use) on `ss` and
 // mark ev_wq[l]; the block's forward waits for that mark.
 int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
     if (P->dry) return ERGM_OK;
@@ -395,7 +396,7 @@ int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
     J.n = 6;
     unsigned* am = w.amax;
     for (int i = 0; i < 6; ++i) {
-        J.j[i] = WqJob{LF(P, l, tens[i]), w.w[i], w.sc[i], am, N[i], K[i], N[i], K[i], 0, 0};
+        J.j[i] = WqJob{LB(P, l, tens[i]), w.w[i], w.sc[i], am, N[i], K[i], N[i], K[i], 0, 0, 1};
         am += N[i];
     }
     ERGM_TRY(quant_weights_fp8(J, ss));
@@ -758,7 +759,7 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
             if (hipMemsetAsync(P->capkv_amax, 0, (size_t)L2E * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "memset");
             WqJobs J{};
             J.n = 1;
-            J.j[0] = WqJob{p.capkv_w, P->capkv8, P->capkv8_s, P->capkv_amax, L2E, E, L2E, E, 0, 0};
+            J.j[0] = WqJob{p.capkv_w_b, P->capkv8, P->capkv8_s, P->capkv_amax, L2E, E, L2E, E, 0, 0, 1};
             ERGM_TRY(quant_weights_fp8(J, ss));
             ERGM_TRY(quant_rows_fp8(P->cap, ERGM_BF16, P->XE, T, E, P->qcap, E, P->scap, ss));
         }

@@ -70,6 +70,9 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const void* __restrict_
 }
 
 // ---- weights: batched over the matrices of one block (WqJobs in common.h) ------------------------
+__device__ __forceinline__ float load_w(const WqJob& j, size_t idx) {
+    return j.w_bf16 ? bf2f(reinterpret_cast<const __bf16*>(j.W)[idx]) : reinterpret_cast<const float*>(j.W)[idx];
+}
 
 __device__ __forceinline__ int find_job(const WqJobs& J, int bid, bool q) {
     int k = 0;
@@ -90,7 +93,7 @@ __global__ __launch_bounds__(256) void wq_amax_kernel(WqJobs J) {
     const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
     const int k0 = kc * 256, k1 = min(jb.K, k0 + 256);
     float m = 0.f;
-    for (int k = k0 + rg; k < k1; k += 4) m = fmaxf(m, fabsf(jb.W[(size_t)k * jb.ldw + n0 + col]));
+    for (int k = k0 + rg; k < k1; k += 4) m = fmaxf(m, fabsf(load_w(jb, (size_t)k * jb.ldw + n0 + col)));
     red[rg][col] = m;
     __syncthreads();
     if (rg == 0) {
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(256) void wq_quant_kernel(WqJobs J) {
 #pragma unroll 4
     for (int i = 0; i < 16; ++i) {
         const int kk = rg * 16 + i, k = k0 + kk;
-        const float w = k < jb.K ? jb.W[(size_t)k * jb.ldw + n0 + col] : 0.f;
+        const float w = k < jb.K ? load_w(jb, (size_t)k * jb.ldw + n0 + col) : 0.f;
         tile[col * LD + kk] = fp8x1(w / s);
     }
     __syncthreads();
@@ -166,13 +169,15 @@ extern "C" int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows
     return quant_rows_fp8(X, x_dtype, ldx, rows, cols, Q, ldq, scale, as_stream(stream));
 }
 
-extern "C" int ergm_quant_weight_fp8(const float* W, int ldw, int K, int N, void* Wt, int ldt, float* scale,
-                                     void* amax_ws, void* stream) {
+extern "C" int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K, int N, void* Wt, int ldt,
+                                     float* scale, void* amax_ws, void* stream) {
     ERGM_CHECK_ARG(amax_ws, "quant_weight_fp8: amax workspace (N x 4 bytes) required");
+    ERGM_CHECK_ARG(w_dtype == ERGM_F32 || w_dtype == ERGM_BF16, "quant_weight_fp8: bad dtype");
     hipStream_t s = as_stream(stream);
     if (hipMemsetAsync(amax_ws, 0, (size_t)N * 4, s) != hipSuccess) return fail(ERGM_EHIP, "quant_weight_fp8: memset");
     WqJobs J{};
     J.n = 1;
-    J.j[0] = WqJob{W, reinterpret_cast<uint8_t*>(Wt), scale, reinterpret_cast<unsigned*>(amax_ws), ldw, K, N, ldt, 0, 0};
+    J.j[0] = WqJob{W, reinterpret_cast<uint8_t*>(Wt), scale, reinterpret_cast<unsigned*>(amax_ws), ldw, K, N, ldt, 0, 0,
+                   w_dtype == ERGM_BF16};
     return quant_weights_fp8(J, s);
 }

@@ -85,13 +85,14 @@ def quant_rows_fp8(X: torch.Tensor, cols: Optional[int] = None):
 
 
 def quant_weight_fp8(W: torch.Tensor):
-    """Conv1D weight W f32 [K, N] → (Wt [N, K] e4m3 bytes, scale [N] f32), column-wise scales."""
+    """Conv1D weight W [K, N] (f32 or bf16) → (Wt [N, K] e4m3 bytes, scale [N] f32), column-wise scales."""
     _need_gpu(W)
     K, N = W.shape
     Wt = torch.empty(N, K, dtype=torch.uint8, device=W.device)
     sc = torch.empty(N, dtype=torch.float32, device=W.device)
     ws = torch.empty(N, dtype=torch.int32, device=W.device)
-    L.call("ergm_quant_weight_fp8", _ptr(W), W.stride(0), K, N, _ptr(Wt), K, _ptr(sc), _ptr(ws), _stream(W.device))
+    dt = L.BF16 if W.dtype == torch.bfloat16 else L.F32
+    L.call("ergm_quant_weight_fp8", _ptr(W), dt, W.stride(0), K, N, _ptr(Wt), K, _ptr(sc), _ptr(ws), _stream(W.device))
     return Wt, sc
 
 

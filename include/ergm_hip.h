@@ -110,11 +110,11 @@ int ergm_gemm_f8_tune(int cfg);
  * Q[r][c] = e4m3(clamp(X[r][c] / scale[r], ±448)).  X bf16 or f32 (x_dtype), cols % 8 == 0.       */
 int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq,
                         float* scale, void* stream);
-/* Column-wise e4m3 quantisation of a Conv1D weight W f32 [K][ldw] (in, out) into its transpose
- * Wt [N][ldt] (k contiguous, the B operand of ergm_gemm_f8): scale[n] = max_k |W[k][n]| / 448.
- * amax_ws: N x 4 bytes of workspace.  K, N multiples of 64.                                      */
-int ergm_quant_weight_fp8(const float* W, int ldw, int K, int N, void* Wt, int ldt, float* scale,
-                          void* amax_ws, void* stream);
+/* Column-wise e4m3 quantisation of a Conv1D weight W [K][ldw] (in, out; f32 or bf16 per w_dtype)
+ * into its transpose Wt [N][ldt] (k contiguous, the B operand of ergm_gemm_f8): scale[n] =
+ * max_k |W[k][n]| / 448.  amax_ws: N x 4 bytes of workspace.  K, N multiples of 64.             */
+int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K, int N, void* Wt, int ldt,
+                          float* scale, void* amax_ws, void* stream);
 
 /* Fused attention over head_dim = 64, token-major tensors with head h at columns [64h, 64h+64):
  *   Q[b][s][h*64+d] = q + (b*Sq + s)*ldq + h*64 + d     (likewise K/V with Sk rows, O with ldo)
@@ -223,7 +223,7 @@ typedef struct {
                                * (build-side, config 5: 768-d features into a 1024-d backbone) */
     int fp8;                  /* 1: the forward Conv1D GEMMs of every block (and the caption K/V
                                * GEMM) run on ergm_gemm_f8 with per-row activation / per-column
-                               * weight scales; weights are re-quantised from the f32 master at
+                               * weight scales; weights are re-quantised from the bf16 shadow at
                                * every forward; LM head, backward and optimizer stay bf16/f32 */
 } ergm_model_dims;
 

@@ -8,6 +8,7 @@ per-row activation / per-column weight scales) is held to SURVEY §8(c)'s fp8 lo
 and to gates set from its measured deviation (tools/fp8_parity.py on MI355X, medium geometry: loss rel
 6.3e-4, logits max|d| 0.26 of max|logit| 3.3, gradient rel-L2 median 0.056 / max 0.106, against the bf16
 path's 8e-5 / 0.021 / 0.006 / 0.051): logits max-abs <= 0.12 * max|logit|, every gradient rel-L2 <= 0.2.
+The fp8 weights are re-quantised (from the bf16 shadow) at every forward.
 """
 import pytest
 import torch
@@ -102,25 +103,31 @@ def test_fp8_forward_training_step_matches_oracle(gpu, geom):
 
 
 def test_fp8_weights_follow_the_optimizer(gpu):
-    """The fp8 weight copies are re-quantised from the f32 master at every forward: after an optimizer
-    step the fp8 model's loss tracks the bf16 model's on the same trajectory."""
+    """The fp8 weight copies are re-quantised at every forward: after optimizer steps the trained fp8
+    model's forward is bit-identical to that of a fresh fp8 model loaded with the updated weights, and
+    the loss went down."""
     from ergm_amd.optim import FusedAdamW
     V, E, Lyr, H, Fd = 500, 128, 2, 2, 64
     _, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=25)
+    cfg.fp8 = True
     batch = synthetic_batch(2, 64, n_turns=4, feat_dim=Fd, seed=9, vocab_hi=490, sp1=498, sp2=499, eos=489)
-    losses = {}
-    for fp8 in (False, True):
-        cfg.fp8 = fp8
-        model = GPT2LMHeadModel(cfg, device=gpu)
-        model.load_state_dict(P0, strict=True)
-        opt = FusedAdamW([model.flat], lr=3e-3, model=model)
-        ls = []
-        for _ in range(6):
-            opt.zero_grad()
-            out = _run(model, batch, gpu)
-            opt.step()
-            ls.append(out.loss.item())
-        losses[fp8] = ls
-    assert losses[True][-1] < losses[True][0] - 0.1, losses[True]
-    for a, b in zip(losses[False], losses[True]):
-        assert abs(a - b) <= FP8_LOSS_RTOL * abs(a), (losses[False], losses[True])
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
+    losses = []
+    for _ in range(4):
+        opt.zero_grad()
+        out = _run(model, batch, gpu)
+        opt.step()
+        losses.append(out.loss.item())
+    assert losses[-1] < losses[0] - 0.05, losses
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    args = dict(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+                auds=kw["audio_feat"])
+    with torch.no_grad():
+        trained = model(**args)
+        fresh = GPT2LMHeadModel(cfg, device=gpu)
+        fresh.load_state_dict(model.state_dict(), strict=True)
+        ref = fresh(**args)
+    assert torch.equal(trained.logits, ref.logits) and trained.loss.item() == ref.loss.item()

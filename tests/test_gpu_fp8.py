@@ -38,11 +38,13 @@ def test_quant_rows_bit_exact(gpu, dtype, rows, cols, ld):
     assert torch.equal(q.cpu(), rq)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("K,N", [(1024, 3072), (4096, 1024), (64, 128)])
-def test_quant_weight_bit_exact(gpu, K, N):
+def test_quant_weight_bit_exact(gpu, K, N, dtype):
     g = torch.Generator().manual_seed(K + N)
     W = torch.randn(K, N, generator=g) * 0.02
     W[:, 5] = 0.0
+    W = W.to(dtype)
     Wt, s = ops.quant_weight_fp8(W.to(gpu))
     rq, rs = _ref_rows(W.t().contiguous())
     assert torch.equal(s.cpu(), rs)

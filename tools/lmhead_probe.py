@@ -1,6 +1,6 @@
 """Split the LM-head GEMM's time into a K-proportional main loop and a fixed part (prologue, epilogue
 stores, tail): time [M, K] x [K, N] (MK x NK, bf16 out, the tied-head layout) for several K, HIP-graph
-replayed.  Usage: python tools/lmhead_probe.py [cfg]"""
+replayed.  Usage: python tools/lmhead_probe.py [cfg [M N [--small]]]"""
 import ctypes as C
 import os
 import sys
@@ -45,7 +45,12 @@ def time_gemm(lib, M, N, K, cfg, out_dtype=torch.bfloat16, reps=20):
 def main():
     lib = L.load()
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else -1
-    M, N = 2048, 50304
+    M, N = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (2048, 50304)
+    if "--small" in sys.argv:  # fixed vs K-proportional cost of a small activation GEMM
+        for K in (64, 128, 256, 768, 1536):
+            t = time_gemm(lib, M, N, K, cfg)
+            print(f"M={M} N={N} K={K}: {t:8.2f} us  {2.0 * M * N * K / t / 1e6:7.0f} TF", flush=True)
+        return
     ts = {}
     for K in (768, 1536, 3072):
         ts[K] = time_gemm(lib, M, N, K, cfg)
