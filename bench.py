@@ -55,6 +55,19 @@ CONFIGS = {
 MODELS = {"small": dict(n_embd=768, n_layer=12, n_head=12), "medium": dict(n_embd=1024, n_layer=24, n_head=16)}
 
 
+def pmc_mfma_busy(probe: int, config: str = "c2"):
+    """MFMA busy fraction of the probed kernel from the newest committed MFMA PMC pass
+    (profiles/r*_pmc_mfma.json, written by tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over
+    GRBM_GUI_ACTIVE/8 x 1024 SIMDs).  None when no summary covers the probe."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_mfma.json")))
+    if probe != 1 or config != "c2" or not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f).get("lm_head_fwd")
+    return round(rec["mfma_busy_pct"] / 100.0, 4) if rec else None
+
+
 def flops_per_utterance(S: int, E: int = 768, L: int = 12, V: int = 50260) -> float:
     """3·S·[L·(28E² + 4E²·Sc/S + 2SE + 4ScE) + 2EV] with Sc = S (causal self-attention
     counted at S²/2, cross-attention in full; LN/softmax/CE/AdamW/embedding excluded)."""
@@ -220,6 +233,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": round(achieved, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                     "mfma_busy_pmc": pmc_mfma_busy(args.probe, args.config),
                      "avg_launch_ms": round(probe_ms, 4),
                      "flops_per_launch": probe_flops},
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
