@@ -48,7 +48,8 @@ CONFIGS = {
     "c2": ("small", 128, 5, 16, 768, False,
            "GPT-2-small + audio/visual fusion, MELD-shape (S=128, 5 turns), B=16/GPU"),
     "c4": ("small", 512, 20, 8, 768, False,
-           "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU"),
+           "GPT-2-small + audio/visual fusion, IEMOCAP-shape (S=512, 20 turns), B=8/GPU, larger features: "
+           "BLIP-vision [B,197,768] (row 0 injected) and wav2vec2 [B,400,768] mean-pooled on the GPU each step"),
     "c5": ("medium", 128, 5, 32, 768, True, "GPT-2-medium + 768-d audio/visual features through projection "
            "GEMMs, fp8 (e4m3) forward Conv1D GEMMs, MELD-shape (S=128, 5 turns), B=32/GPU"),
 }
@@ -150,15 +151,22 @@ def main():
     total = args.warmup + args.steps
     sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=int(0.1 * total),
                                                       num_training_steps=total, power=2)
-    batch = synthetic_batch(B, S, n_turns=turns, seed=1000 + rank, feat_dim=Fd)
+    big_feat = args.config == "c4"  # "larger audio/visual feat" (pooling is build-side)
+    batch = synthetic_batch(B, S, n_turns=turns, seed=1000 + rank, feat_dim=Fd, visual_rows=197 if big_feat else 1)
     kw = dict(input_ids=batch["input_ids"], token_type_ids=batch["token_type_ids"], labels=batch["labels"],
               emotion_labels=batch["emotion_labels"], caption_ids=batch["caption_ids"], imgs=batch["visual_feat"],
               auds=batch["audio_feat"])
     kw = {k: v.to(dev) for k, v in kw.items()}  # inputs resident in HBM before timing
+    aud_hidden = None
+    if big_feat:  # wav2vec2-shaped encoder output, pooled inside every timed step
+        from ergm_amd.features import mean_pool
+        aud_hidden = (0.1 * torch.randn(B, 400, Fd, generator=torch.Generator().manual_seed(7 + rank))).to(dev)
     loss_acc = torch.zeros(2, device=dev)
     correct = torch.zeros(1, device=dev, dtype=torch.int64)
 
     def step():
+        if aud_hidden is not None:
+            kw["auds"] = mean_pool(aud_hidden)
         out = model(**kw)
         opt.zero_grad()
         out.loss.backward()

@@ -73,6 +73,7 @@ _SIGS = {
     "ergm_colsum_workspace_size": (sz, [i32, i32]),
     "ergm_colsum": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
     "ergm_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "ergm_feat_pool": (i32, [vp, i32, i32, i32, i32, C.c_long, C.c_long, vp, vp, i32, vp]),
     "ergm_embed_bwd_workspace_size": (sz, [i32]),
     "ergm_embed_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, vp]),
     "ergm_count_valid": (i32, [vp, i32, i32, vp, vp]),

@@ -423,3 +423,48 @@ int proj_grad_pack(const float* dh0, void* d, int B, int Bp, int S, int E, hipSt
 }
 
 }  // namespace ergm
+
+// ---- feature pooling (data_process/feature_extraction.py:63,69) -------------
+// out[b][d] = mean over the valid frames t < len_b of x[b][t][d]: the torch.mean(last_hidden_state,
+// dim=1) the reference applies offline to wav2vec2 (audio) and BLIP-vision (keyframe) encoder outputs,
+// on the GPU, with optional per-sample lengths for padded audio.  Block = 64 feature columns x 4 frame
+// groups (coalesced 64-column rows); the 4 partial sums are combined in a fixed order (deterministic).
+namespace ergm {
+template <bool BF16>
+__global__ __launch_bounds__(256) void feat_pool_kernel(const void* __restrict__ x, int T, int D, long ld_t,
+                                                        long ld_b, const int* __restrict__ lengths,
+                                                        float* __restrict__ out, int ld_out) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y, col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int d = blockIdx.x * 64 + col;
+    const int n = lengths ? max(0, min(T, lengths[b])) : T;
+    float s = 0.f;
+    if (d < D) {
+        for (int t = rg; t < n; t += 4) {
+            const size_t i = (size_t)b * ld_b + (size_t)t * ld_t + d;
+            s += BF16 ? bf2f(reinterpret_cast<const __bf16*>(x)[i]) : reinterpret_cast<const float*>(x)[i];
+        }
+    }
+    red[rg][col] = s;
+    __syncthreads();
+    if (rg == 0 && d < D) {
+        const float tot = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+        out[(size_t)b * ld_out + d] = n > 0 ? tot / (float)n : 0.f;
+    }
+}
+}  // namespace ergm
+
+extern "C" int ergm_feat_pool(const void* x, int x_dtype, int B, int T, int D, long ld_t, long ld_b,
+                              const int* lengths, float* out, int ld_out, void* stream) {
+    using namespace ergm;
+    ERGM_CHECK_ARG(x && out && B > 0 && T > 0 && D > 0 && ld_t >= D && ld_b >= (long)T * ld_t && ld_out >= D,
+                   "feat_pool: bad shape");
+    ERGM_CHECK_ARG(x_dtype == ERGM_F32 || x_dtype == ERGM_BF16, "feat_pool: bad dtype");
+    dim3 grid(cdiv(D, 64), B);
+    hipStream_t s = as_stream(stream);
+    if (x_dtype == ERGM_BF16)
+        hipLaunchKernelGGL(feat_pool_kernel<true>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
+    else
+        hipLaunchKernelGGL(feat_pool_kernel<false>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
+    return check_launch("feat_pool");
+}

@@ -99,8 +99,13 @@ class KVCacheGenerator:
         if S0 >= self.max_len:
             raise ValueError("prompt longer than max_len")
         wte, wpe = self._f("__wte_pad"), self._f("transformer.wpe.weight")
-        vis = None if imgs is None else imgs.float().reshape(1, -1, self.E)
-        aud = None if auds is None else auds.float().reshape(1, self.E)
+        Fd = self.m.layout.Fd
+        vis = None if imgs is None else imgs.float().reshape(1, -1, Fd)[:, 0]
+        aud = None if auds is None else auds.float().reshape(1, Fd)
+        if vis is not None and Fd != self.E:  # config 5: the build-side projections (Conv1D), MFMA GEMMs
+            vis, aud = (ops.gemm(x.to(torch.bfloat16), self._b(f"transformer.{m}.weight"), 1, self.E, Fd, L.MK, L.KN,
+                                 out_dtype=torch.float32, epilogue=L.EPI_BIAS, bias=self._f(f"transformer.{m}.bias"))
+                        for x, m in ((vis, "visual_proj"), (aud, "audio_proj")))
         h, _ = ops.embed_fwd(input_ids, token_type_ids, input_ids, wte, wpe, vis, aud)
         _, cap = ops.embed_fwd(caption_ids, None, caption_ids, wte, wpe)
         Sc = caption_ids.shape[1]

@@ -175,6 +175,23 @@ def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None):
     return h0, cap
 
 
+def feat_pool(x: torch.Tensor, lengths: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """Mean over frames of encoder outputs x [B, T, D] (f32 / bf16, any row strides with unit
+    last-dim stride) -> [B, D] f32; ``lengths`` [B] int32 limits each sample to its valid frames."""
+    _need_gpu(x)
+    if x.dim() != 3 or x.stride(2) != 1:
+        raise ValueError("feat_pool expects [B, T, D] with contiguous feature rows")
+    B, T, D = x.shape
+    if out is None:
+        out = torch.empty(B, D, dtype=torch.float32, device=x.device)
+    if lengths is not None:
+        lengths = lengths.to(x.device, torch.int32).contiguous()
+    dt = L.BF16 if x.dtype == torch.bfloat16 else L.F32
+    L.call("ergm_feat_pool", _ptr(x), dt, B, T, D, x.stride(1), x.stride(0), _ptr(lengths), _ptr(out), out.stride(0),
+           _stream(x.device))
+    return out
+
+
 def embed_bwd(ids, tt, cap_ids, dh0, dcap, dwte, dwpe):
     B, S = ids.shape
     V, E = dwte.shape

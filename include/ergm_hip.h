@@ -155,6 +155,12 @@ int ergm_colsum(const void* X, int x_dtype, int rows, int cols, int ldx, float* 
 int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
                    const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0,
                    void* cap, int B, int S, int E, int V, void* stream);
+/* Feature pooling (data_process/feature_extraction.py:63,69: torch.mean(last_hidden_state, dim=1) of the
+ * wav2vec2 / BLIP-vision encoder outputs): out[b][d] = mean_{t < len_b} x[b][t][d], x f32 or bf16 with
+ * strides ld_t (frames) and ld_b (samples) in elements, lengths optional (NULL = all T frames; padded
+ * audio otherwise), out f32 [B][ld_out].  Fixed summation order (deterministic).                   */
+int ergm_feat_pool(const void* x, int x_dtype, int B, int T, int D, long ld_t, long ld_b,
+                   const int* lengths, float* out, int ld_out, void* stream);
 /* Deterministic (sorted segment-sum) embedding backward:
  *   dwte[v] += Σ_{t: ids[t]=v} dh0[t] + Σ_{t: tt[t]=v} dh0[t] + Σ_{t: cap[t]=v} dcap[t]
  *   dwpe[s]  = Σ_b dh0[b,s]

@@ -14,23 +14,27 @@ V, E, LYR, H, P = 500, 128, 2, 2, 64
 LOGIT_ATOL = 0.06
 
 
-def _setup(gpu):
-    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P)
+def _setup(gpu, feat_dim=None):
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P, feat_dim=feat_dim)
     P0 = O.init_params(ocfg, seed=11)
-    model = GPT2LMHeadModel(ERGMConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P), device=gpu)
-    model.load_state_dict(P0, strict=False)
+    model = GPT2LMHeadModel(ERGMConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P,
+                                       feat_dim=feat_dim), device=gpu)
+    model.load_state_dict(P0, strict=True)
     return ocfg, P0, model
 
 
-def test_decode_steps_match_full_recompute(gpu):
-    ocfg, P0, model = _setup(gpu)
+@pytest.mark.parametrize("feat_dim", [None, 64])
+def test_decode_steps_match_full_recompute(gpu, feat_dim):
+    """feat_dim=64: the config-5 projections of the prompt's visual / audio vectors (E=128)."""
+    ocfg, P0, model = _setup(gpu, feat_dim)
+    Fd = feat_dim or E
     g = torch.Generator().manual_seed(4)
     S0 = 12
     ids = torch.randint(0, 490, (1, S0), generator=g)
     tt = torch.full((1, S0), 498)
     tt[:, 6:] = 499
     cap = torch.randint(0, 490, (1, S0), generator=g)
-    vis, aud = 0.1 * torch.randn(1, E, generator=g), 0.1 * torch.randn(1, E, generator=g)
+    vis, aud = 0.1 * torch.randn(1, Fd, generator=g), 0.1 * torch.randn(1, Fd, generator=g)
     gen = KVCacheGenerator(model, max_len=32)
     logits = gen.prefill(ids.to(gpu), tt.to(gpu), cap.to(gpu), vis.to(gpu), aud.to(gpu))
     forced = torch.randint(0, 490, (6,), generator=g)
