@@ -124,12 +124,20 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    # rehearsal hook (one-GPU box): ERGM_BENCH_REHEARSE=1 puts every rank on cuda:0 and uses gloo, so the
+    # data-parallel path of this script runs end to end without a GPU per rank (numbers not meaningful)
+    rehearse = os.environ.get("ERGM_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         pg = dist.group.WORLD
 
     from ergm_amd import _lib
