@@ -17,6 +17,8 @@ from ergm_amd import _lib as L  # noqa: E402
 T, E, F, LYR, VP = 2048, 768, 3072, 12, 50304
 if "--c5" in sys.argv:  # config 5 geometry (GPT-2-medium, B=32, S=128); its forward GEMMs run fp8
     T, E, F, LYR = 4096, 1024, 4096, 24
+if "--c4" in sys.argv:  # config 4 geometry (GPT-2-small, B=8, S=512)
+    T = 4096
 L2E = 2 * E * LYR
 MK, KM, NK, KN = L.MK, L.KM, L.NK, L.KN
 BF, FP = L.BF16, L.F32
@@ -90,8 +92,11 @@ def main():
     total_best = 0.0
     total_auto = 0.0
     only_bwd = "--c5" in sys.argv
+    only_dw = "--dw" in sys.argv
     for (name, cnt, M, N, K, al, lda, bl, ldb, epi, cdt) in SHAPES:
         if only_bwd and name.startswith("fwd") and name != "fwd lm_head":
+            continue
+        if only_dw and al != KM:
             continue
         a_rows = M if al == MK else K
         b_rows = N if bl == NK else K
