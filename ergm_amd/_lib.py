@@ -58,6 +58,8 @@ _SIGS = {
     "ergm_version": (i32, []),
     "ergm_last_error": (i32, [C.c_char_p, sz]),
     "ergm_gemm_tune": (i32, [i32, i32]),
+    "ergm_gemm_set_override": (i32, [i32, i32, i32, i32, i32, i32, i32]),
+    "ergm_gemm_trace": (i32, [i32, vp, i32]),
     "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
     "ergm_gemm_f8": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, vp, vp]),

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "common.h"
 #include "tiles.h"
@@ -580,11 +581,78 @@ static bool pipe_ok(const ergm_gemm_desc* d) {
            (!d->aux_out || d->ld_aux_out % 8 == 0);
 }
 
+// Per-shape configuration overrides (ergm_gemm_set_override): measured in the running training step
+// (tools/step_tune.py), where per-kernel isolated timings do not predict the concurrent step.  Keyed on
+// (M, N, K, layouts); a small fixed table, written from the host only (plan creation / tuning).
+struct GemmOverride {
+    int M, N, K, al, bl, cfg, split;
+};
+static constexpr int kMaxOverrides = 64;
+static GemmOverride g_over[kMaxOverrides];
+static int g_n_over = 0;
+static std::mutex g_over_mu;
+
+// Built-in entries measured by tools/step_tune.py inside the bench step (interleaved A/B against the
+// automatic choice; profiles/r01_step_tune_*.json).  Runtime overrides take precedence.
+static constexpr GemmOverride kStepTuned[] = {
+    // config 2 (GPT-2-small, B=16, S=128; forward GEMMs run per batch half, M = 1024)
+    {3073, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient
+    {769, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient
+    {1024, 2304, 768, ERGM_MK, ERGM_KN, 3, 1},   // c_attn forward
+    {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
+    {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
+    {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+};
+
+static bool find_override(const ergm_gemm_desc* d, int& cfg, int& split) {
+    std::lock_guard<std::mutex> lk(g_over_mu);
+    for (int i = 0; i < g_n_over; ++i) {
+        const GemmOverride& o = g_over[i];
+        if (o.M == d->M && o.N == d->N && o.K == d->K && o.al == d->a_layout && o.bl == d->b_layout) {
+            cfg = o.cfg;
+            split = o.split;
+            return true;
+        }
+    }
+    for (const GemmOverride& o : kStepTuned) {
+        if (o.M == d->M && o.N == d->N && o.K == d->K && o.al == d->a_layout && o.bl == d->b_layout) {
+            cfg = o.cfg;
+            split = o.split;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Shape trace (ergm_gemm_trace): the distinct (M, N, K, layouts) of the ergm_gemm calls since enabled.
+static bool g_trace_on = false;
+static int g_trace[256][5];
+static int g_trace_n = 0;
+
+static void trace_shape(const ergm_gemm_desc* d) {
+    std::lock_guard<std::mutex> lk(g_over_mu);
+    if (!g_trace_on) return;
+    for (int i = 0; i < g_trace_n; ++i)
+        if (g_trace[i][0] == d->M && g_trace[i][1] == d->N && g_trace[i][2] == d->K && g_trace[i][3] == d->a_layout &&
+            g_trace[i][4] == d->b_layout)
+            return;
+    if (g_trace_n < 256) {
+        int* t = g_trace[g_trace_n++];
+        t[0] = d->M; t[1] = d->N; t[2] = d->K; t[3] = d->a_layout; t[4] = d->b_layout;
+    }
+}
+
 static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
     GemmPlan p;
     const int M = d->M, N = d->N, K = d->K;
     int split = 1;
-    if (!pipe_ok(d) || !combo_ok(d->a_layout == ERGM_KM, d->b_layout == ERGM_KN, d->epilogue, d->c_dtype == ERGM_BF16)) {
+    int ocfg = -1, osplit = 1;
+    const bool pipe = pipe_ok(d) &&
+                      combo_ok(d->a_layout == ERGM_KM, d->b_layout == ERGM_KN, d->epilogue, d->c_dtype == ERGM_BF16);
+    if (pipe && g_force_cfg < 0 && d->split_k == 0 && find_override(d, ocfg, osplit)) {
+        p.cfg = ocfg;
+        split = osplit;
+    } else if (!pipe) {
         p.cfg = -1;
         const long t128 = tiles_of(M, N, 128, 128), t64 = tiles_of(M, N, 64, 64);
         p.bm = p.bn = t128 >= 240 ? 128 : 64;
@@ -857,6 +925,39 @@ extern "C" size_t ergm_gemm_workspace_size(const ergm_gemm_desc* d) {
     return (size_t)p.split * d->M * d->N * sizeof(float);
 }
 
+extern "C" int ergm_gemm_set_override(int M, int N, int K, int a_layout, int b_layout, int cfg, int split) {
+    ERGM_CHECK_ARG(cfg >= -1 && cfg < kNumCfgs && split >= 1 && split <= 16, "gemm_set_override: cfg in [-1, %d)",
+                   kNumCfgs);
+    std::lock_guard<std::mutex> lk(g_over_mu);
+    for (int i = 0; i < g_n_over; ++i) {
+        GemmOverride& o = g_over[i];
+        if (o.M == M && o.N == N && o.K == K && o.al == a_layout && o.bl == b_layout) {
+            if (cfg < 0) {
+                o = g_over[--g_n_over];
+            } else {
+                o.cfg = cfg;
+                o.split = split;
+            }
+            return ERGM_OK;
+        }
+    }
+    if (cfg < 0) return ERGM_OK;
+    ERGM_CHECK_ARG(g_n_over < kMaxOverrides, "gemm_set_override: table full");
+    g_over[g_n_over++] = GemmOverride{M, N, K, a_layout, b_layout, cfg, split};
+    return ERGM_OK;
+}
+
+extern "C" int ergm_gemm_trace(int on, int* shapes, int max_shapes) {
+    std::lock_guard<std::mutex> lk(g_over_mu);
+    const int n = g_trace_n;
+    if (shapes)
+        for (int i = 0; i < n && i < max_shapes; ++i)
+            for (int j = 0; j < 5; ++j) shapes[i * 5 + j] = g_trace[i][j];
+    if (on && !g_trace_on) g_trace_n = 0;
+    g_trace_on = on != 0;
+    return n;
+}
+
 extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, void* C, void* ws,
                          size_t ws_bytes, void* stream) {
     ERGM_CHECK_ARG(d && A && B && C, "ergm_gemm: null argument");
@@ -880,6 +981,7 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     ERGM_CHECK_ARG(!(e == ERGM_EPI_BIAS_RESID || e == ERGM_EPI_GELU_BWD) || d->aux, "ergm_gemm: epilogue needs aux");
     ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || d->aux_out, "ergm_gemm: BIAS_GELU needs aux_out");
 
+    trace_shape(d);
     GemmPlan p = plan_gemm(d);
     GemmArgs a;
     a.A = reinterpret_cast<const __bf16*>(A);

@@ -92,6 +92,14 @@ typedef struct {
  * LDS stages, see kCfgs in ergm_amd/csrc/gemm.hip) and split-K count for later ergm_gemm calls;
  * cfg = -1 restores the automatic choice.  Used by tools/gemm_tune.py.                          */
 int ergm_gemm_tune(int cfg, int split);
+/* Per-shape override of the automatic choice: GEMMs of exactly (M, N, K, a_layout, b_layout) with
+ * split_k == 0 use configuration `cfg` and `split`; cfg = -1 removes the entry.  Process-wide, set
+ * before the plans that use it are created (their workspace is sized then).  ergm_gemm_trace(on,
+ * shapes, max) records the distinct shapes of later ergm_gemm calls (on = 1 starts a new record) and
+ * returns how many were recorded so far, copying up to `max` of them as 5 ints (M, N, K, layouts).
+ * Both serve tools/step_tune.py, which measures configurations inside the running training step. */
+int ergm_gemm_set_override(int M, int N, int K, int a_layout, int b_layout, int cfg, int split);
+int ergm_gemm_trace(int on, int* shapes, int max_shapes);
 /* Workspace bytes ergm_gemm needs for `desc` (split-K partial slabs); 0 if none. */
 size_t ergm_gemm_workspace_size(const ergm_gemm_desc* desc);
 int ergm_gemm(const ergm_gemm_desc* desc, const void* A, const void* B, void* C, void* workspace,
