@@ -11,12 +11,19 @@
 // lane holds 16 keys of ONE query: row max/sum are lane-local + two xor-shuffles.  The output is also
 // kept transposed, Oᵀ = Vᵀ·Pᵀ: P feeds the MFMA B operand straight from registers (k-order
 // permuted identically on both operands) and Vᵀ comes from the LDS V tile by ds_read_b64_tr_b16.
-// Backward: dK/dV kernel (workgroup = 64 keys, loops over query tiles, P recomputed from the
-// forward LSE) + dQ kernel (workgroup = 64 queries, loops over key tiles); no atomics, deterministic.
+// Backward: δ = rowsum(dO·O) kernel, dK/dV kernel (workgroup = 64 keys, loops over query tiles, P
+// recomputed from the forward LSE) + dQ kernel (workgroup = 64 queries, loops over key tiles); no
+// atomics, deterministic.  The tiled kernels stream their 64-row tiles through a 3-stage LDS ring filled
+// by LDS-DMA (tiles.h GldsTile: two tiles in flight while one is consumed, one barrier per tile); causal
+// grids start with the longest rows.
 // Sequences of at most 128 (the training path: S = 128 tokens, 128 caption rows) take the
 // *_short kernels instead: one 8-wave workgroup per (b, h) holding every operand in LDS, the whole
 // backward in one launch.  Both paths evaluate every product in the same order (bit-identical).
+// Softmax arithmetic in the exp2 domain (v_exp_f32 is 2^x): exp(scale·s − shift) = exp2(fma(s, c, −shift·log2e))
+// with c = scale·log2e, one FMA + one v_exp per score; tiles a wave sees entirely unmasked (uniform
+// test per wave and tile) skip the mask compares.
 #include "common.h"
+#include "tiles.h"
 
 namespace ergm {
 
@@ -27,18 +34,6 @@ constexpr int AT_TILE_BYTES = AT_T * AT_D * 2;  // 8 KiB
 // 64x64 bf16 tile in LDS, 128-B rows, 16-B chunk c of row r stored at chunk c ^ (r & 7):
 // conflict-free for both ds_read_b128 row reads and the ds_read_b64_tr_b16 reads below.
 __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-
-// Stage rows [row0, row0+64) of a token-major tensor (row stride ld, head column offset col0).
-__device__ __forceinline__ void stage_tile(char* lds, const __bf16* base, int ld, int row0, int nrows, int col0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        int c = threadIdx.x + i * 256;
-        int r = c >> 3, ch = c & 7;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (row0 + r < nrows) v = *reinterpret_cast<const uint4*>(base + (size_t)(row0 + r) * ld + col0 + ch * 8);
-        *reinterpret_cast<uint4*>(lds + tile_off(r, ch)) = v;
-    }
-}
 
 // Row-read operand fragment (16x16x32): lane l gets X[row0 + (l&15)][32ks + 8(l>>4) + j].
 __device__ __forceinline__ bf16x8 row_frag(const char* lds, int row0, int ks) {
@@ -93,10 +88,19 @@ struct AttnArgs {
     float scale;
 };
 
+constexpr float AT_LOG2E = 1.4426950408889634f;
+
+// exp(scale·s − shift) given c = scale·log2e and shift2 = shift·log2e.
+__device__ __forceinline__ float exp_sc(float s, float c, float shift2) {
+    return __builtin_amdgcn_exp2f(fmaf(s, c, -shift2));
+}
+
 // One 64-key tile of the online-softmax forward for this lane's query q (keys key0..key0+63 of the
-// staged sK / sV tiles): scores, running max / sum update, Oᵀ += Vᵀ·Pᵀ.
-template <bool CAUSAL>
-__device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int key0, int q, int Sk, float scale,
+// staged sK / sV tiles): scores, running max / sum update, Oᵀ += Vᵀ·Pᵀ.  m is the running max of the
+// RAW scores (before the 1/sqrt(d) scale).  MASK=false: every key of the tile is valid for every query
+// of the wave.
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int key0, int q, int Sk, float c,
                                             const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l) {
     const int g = (threadIdx.x & 63) >> 4;
     f32x4 s[4];
@@ -112,24 +116,26 @@ __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int 
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            int key = key0 + kb * 16 + 4 * g + r;
-            float x = s[kb][r] * scale;
-            bool masked = key >= Sk || (CAUSAL && key > q);
-            x = masked ? -INFINITY : x;
-            s[kb][r] = x;
+            float x = s[kb][r];
+            if (MASK) {
+                const int key = key0 + kb * 16 + 4 * g + r;
+                const bool masked = key >= Sk || (CAUSAL && key > q);
+                x = masked ? -INFINITY : x;
+                s[kb][r] = x;
+            }
             mx = fmaxf(mx, x);
         }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mnew = fmaxf(m, mx);
-    const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = __expf(m - muse);
+    const float m2 = (mnew == -INFINITY ? 0.f : mnew) * c;
+    const float alpha = exp_sc(m, c, m2);
     float rs = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float p = __expf(s[kb][r] - muse);
+            float p = exp_sc(s[kb][r], c, m2);
             s[kb][r] = p;
             rs += p;
         }
@@ -148,7 +154,20 @@ __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int 
     }
 }
 
-// Normalised output row (bf16) and the log-sum-exp of this lane's query.
+// Keys key0..key0+63 against the wave's queries qw0..qw0+15: does any pair need the mask?
+template <bool CAUSAL>
+__device__ __forceinline__ bool tile_masked(int key0, int Sk, int qw0) {
+    return key0 + AT_T > Sk || (CAUSAL && key0 + AT_T - 1 > qw0);
+}
+
+template <bool CAUSAL>
+__device__ __forceinline__ void fwd_tile(const char* sK, const char* sV, int key0, int q, int qw0, int Sk, float c,
+                                         const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l) {
+    if (tile_masked<CAUSAL>(key0, Sk, qw0)) fwd_kv_tile<CAUSAL, true>(sK, sV, key0, q, Sk, c, qf, o, m, l);
+    else fwd_kv_tile<CAUSAL, false>(sK, sV, key0, q, Sk, c, qf, o, m, l);
+}
+
+// Normalised output row (bf16) and the log-sum-exp (natural log, scaled scores) of this lane's query.
 __device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q, const f32x4 (&o)[4], float m,
                                           float l) {
     const int g = (threadIdx.x & 63) >> 4;
@@ -162,18 +181,164 @@ __device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q
         for (int r = 0; r < 4; ++r) w[r] = f2bf(o[d][r] * inv);
         *reinterpret_cast<bf16x4*>(Ob + d * 16 + 4 * g) = w;
     }
-    if (g == 0) a.lse[((size_t)b * a.H + h) * a.Sq + q] = m + logf(l);
+    if (g == 0) a.lse[((size_t)b * a.H + h) * a.Sq + q] = m * a.scale + logf(l);
+}
+
+// dK/dV contribution of one 64-query tile (Q, dO, LSE, δ staged) for this lane's key: P recomputed,
+// dS = P∘(dP − δ); dVᵀ += dOᵀ·Pᵀ, dKᵀ += Qᵀ·dSᵀ.  tS (optional): dS also stored key-major, bf16, at
+// tile row krow (the fused short backward reuses it for dQ).  MASK=false: no pair of the tile is masked.
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
+                                         int key, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
+                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow) {
+    const int g = (threadIdx.x & 63) >> 4;
+    f32x4 p[4], ds[4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+        s = MFMA16(row_frag(sQ, qb * 16, 0), kf[0], s);
+        s = MFMA16(row_frag(sQ, qb * 16, 1), kf[1], s);
+        f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp = MFMA16(row_frag(sdO, qb * 16, 0), vf[0], dp);
+        dp = MFMA16(row_frag(sdO, qb * 16, 1), vf[1], dp);
+        // element r: query q0 + qb*16 + 4g + r, key `key`
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ql = qb * 16 + 4 * g + r;
+            float pv = exp_sc(s[r], c, sL[ql] * AT_LOG2E);
+            if (MASK) {
+                const int qq = q0 + ql;
+                const bool masked = qq >= Sq || key >= Sk || (CAUSAL && key > qq);
+                pv = masked ? 0.f : pv;
+            }
+            p[qb][r] = pv;
+            ds[qb][r] = pv * (dp[r] - sD[ql]);
+        }
+        if (tS) {  // dS[key][q..q+3] -> key-major LDS tile (one 8-byte store per lane)
+            bf16x4 w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = f2bf(ds[qb][r]);
+            const int qc = qb * 16 + 4 * g;  // query column inside the tile
+            *reinterpret_cast<bf16x4*>(tS + tile_off(krow, qc >> 3) + (qc & 7) * 2) = w;
+        }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        bf16x8 pb = pack_p(p[2 * half], p[2 * half + 1]);
+        bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            dv[d] = MFMA16(tr_frag(sdO, 32 * half, d * 16), pb, dv[d]);
+            dk[d] = MFMA16(tr_frag(sQ, 32 * half, d * 16), sb, dk[d]);
+        }
+    }
+}
+
+// Queries q0..q0+63 against the wave's keys kw0..kw0+15: does any pair need the mask?
+template <bool CAUSAL>
+__device__ __forceinline__ bool dkv_masked(int q0, int Sq, int kw0, int Sk) {
+    return q0 + AT_T > Sq || kw0 + 16 > Sk || (CAUSAL && kw0 + 15 > q0);
+}
+
+template <bool CAUSAL>
+__device__ __forceinline__ void dkv_step(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
+                                         int key, int kw0, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
+                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow) {
+    if (dkv_masked<CAUSAL>(q0, Sq, kw0, Sk))
+        dkv_tile<CAUSAL, true>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow);
+    else
+        dkv_tile<CAUSAL, false>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow);
+}
+
+// dQ contribution of one 64-key tile for this lane's query (lq2 = LSE·log2e, dl = δ).
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dq_tile(const char* sK, const char* sV, int key0, int q, int Sq, int Sk, float c,
+                                        float lq2, float dl, const bf16x8 (&qf)[2], const bf16x8 (&dof)[2],
+                                        f32x4 (&dq)[4]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    f32x4 ds[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+        s = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s);
+        s = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s);
+        f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp = MFMA16(row_frag(sV, kb * 16, 0), dof[0], dp);
+        dp = MFMA16(row_frag(sV, kb * 16, 1), dof[1], dp);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float pv = exp_sc(s[r], c, lq2);
+            if (MASK) {
+                const int key = key0 + kb * 16 + 4 * g + r;
+                const bool masked = key >= Sk || q >= Sq || (CAUSAL && key > q);
+                pv = masked ? 0.f : pv;
+            }
+            ds[kb][r] = pv * (dp[r] - dl);
+        }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) dq[d] = MFMA16(tr_frag(sK, 32 * half, d * 16), sb, dq[d]);
+    }
+}
+
+// Tile of a tiled-kernel workgroup, XCD-aware: workgroups are dispatched round-robin over the 8 XCDs
+// (linear id mod 8), so the (b, h) pairs are split into 8 contiguous groups, one per XCD, and all row
+// blocks of a pair run on the XCD whose L2 holds that pair's K/V (or Q/dO); within an XCD, row block 0
+// of every pair is dispatched first (callers map it to the longest causal rows).
+struct AttnBlock {
+    int x, h, b;
+};
+__device__ __forceinline__ AttnBlock attn_block() {
+    const int nx = gridDim.x, P = gridDim.y * gridDim.z;
+    AttnBlock r;
+    if ((P & 7) == 0) {
+        const int L = blockIdx.x + nx * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int per = P >> 3, j = L >> 3;
+        const int pair = (L & 7) * per + j % per;
+        r.x = j / per;
+        r.h = pair % gridDim.y;
+        r.b = pair / gridDim.y;
+    } else {
+        r.x = blockIdx.x;
+        r.h = blockIdx.y;
+        r.b = blockIdx.z;
+    }
+    return r;
+}
+
+constexpr int AR_NS = 3;                       // LDS ring stages of the tiled kernels
+using AttnTile = GldsTile<AT_T, false, 4>;      // one 64x64 bf16 tile: 2 LDS-DMA wave-instructions per wave
+
+// Make the compiler wait for a register operand loaded before the ring prologue: its own vmcnt wait then
+// sits here, not inside the loop (where it would drain the untracked LDS-DMA ring every iteration).
+__device__ __forceinline__ void vm_ready(const bf16x8& x) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    asm volatile("" ::"v"(__builtin_bit_cast(u32x4, x)));
+}
+__device__ __forceinline__ void vm_ready(float x) { asm volatile("" ::"v"(x)); }
+
+// Ring step: wait until this wave's DMA for the current stage landed (`after` younger stages may stay in
+// flight), finish this wave's LDS reads of the slot about to be refilled, then one workgroup barrier.
+template <int LPS>
+__device__ __forceinline__ void ring_sync(int after) {
+    wait_stages<LPS, AR_NS - 2>(after);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 }
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char sK[AT_TILE_BYTES];
-    __shared__ __attribute__((aligned(16))) char sV[AT_TILE_BYTES];
-    const int b = blockIdx.z, h = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char ring[AR_NS * 2 * AT_TILE_BYTES];  // [stage][K|V]
+    const AttnBlock blk = attn_block();
+    const int b = blk.b, h = blk.h;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i16 = lane & 15, g = lane >> 4;
-    const int qblk = blockIdx.x * AT_T;
+    const int qblk = (CAUSAL ? gridDim.x - 1 - blk.x : blk.x) * AT_T;
     const int q = qblk + wave * 16 + i16;  // this lane's query
+    const float c = a.scale * AT_LOG2E;
     const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
     const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
@@ -182,6 +347,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     bf16x8 qf[2];
     qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
     qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
+    vm_ready(qf[0]);
+    vm_ready(qf[1]);
 
     f32x4 o[4];
 #pragma unroll
@@ -193,54 +360,67 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         int qlast = min(a.Sq, qblk + AT_T) - 1;
         nkt = min(nkt, qlast / AT_T + 1);
     }
+    auto issue = [&](int kt) {
+        char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
+        AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
+    };
+    for (int s = 0; s < AR_NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
-        const int key0 = kt * AT_T;
-        __syncthreads();
-        stage_tile(sK, Kb, a.ldk, key0, a.Sk, 0);
-        stage_tile(sV, Vb, a.ldv, key0, a.Sk, 0);
-        __syncthreads();
-        fwd_kv_tile<CAUSAL>(sK, sV, key0, q, a.Sk, a.scale, qf, o, m, l);
+        ring_sync<4>(min(AR_NS - 2, nkt - 1 - kt));
+        if (kt + AR_NS - 1 < nkt) issue(kt + AR_NS - 1);
+        const char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        fwd_tile<CAUSAL>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l);
     }
     fwd_store(a, b, h, q, o, m, l);
 }
 
-// delta[b,h,q] = Σ_d dO·O
+// δ[b,h,q] = Σ_d dO·O: 4 threads per (token, head), 16 dims each, partials combined (p0+p1)+(p2+p3) —
+// the order attn_bwd_short_kernel uses, so both backward paths see bit-identical δ.
 __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
-    const size_t n = (size_t)a.B * a.Sq * a.H;
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    int h = (int)(i % a.H);
-    size_t tok = i / a.H;  // b*Sq + q
-    const __bf16* dO = a.dout + tok * a.lddo + h * AT_D;
-    const __bf16* O = a.o + tok * a.ldo + h * AT_D;
+    const size_t n = (size_t)a.B * a.Sq * a.H * 4;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int part = (int)(i & 3);
+    const size_t row = i >> 2;  // (b*Sq + q)*H + h
+    const int h = (int)(row % a.H);
+    const size_t tok = row / a.H;
     float s = 0.f;
+    if (i < n) {
+        const __bf16* dd = a.dout + tok * a.lddo + h * AT_D + part * 16;
+        const __bf16* od = a.o + tok * a.ldo + h * AT_D + part * 16;
+        const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(dd), x1 = *reinterpret_cast<const bf16x8*>(dd + 8);
+        const bf16x8 y0 = *reinterpret_cast<const bf16x8*>(od), y1 = *reinterpret_cast<const bf16x8*>(od + 8);
 #pragma unroll
-    for (int c = 0; c < AT_D; c += 8) {
-        bf16x8 x = *reinterpret_cast<const bf16x8*>(dO + c);
-        bf16x8 y = *reinterpret_cast<const bf16x8*>(O + c);
+        for (int j = 0; j < 8; ++j) s += bf2f(x0[j]) * bf2f(y0[j]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += bf2f(x[j]) * bf2f(y[j]);
+        for (int j = 0; j < 8; ++j) s += bf2f(x1[j]) * bf2f(y1[j]);
     }
-    int b = (int)(tok / a.Sq), q = (int)(tok % a.Sq);
-    a.delta[((size_t)b * a.H + h) * a.Sq + q] = s;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (i < n && part == 0) {
+        const int bb = (int)(tok / a.Sq), q = (int)(tok % a.Sq);
+        a.delta[((size_t)bb * a.H + h) * a.Sq + q] = s;
+    }
 }
 
-// dK, dV: workgroup = 64 keys of one (b, h), each wave 16 keys; loop over query tiles.
+// dK, dV: workgroup = 64 keys of one (b, h), each wave 16 keys; loop over query tiles.  A ring stage holds
+// the Q and dO tiles and the tile's 64 LSE and δ values (one 256-B DMA per wave: waves 0/2 LSE, 1/3 δ).
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char sQ[AT_TILE_BYTES];
-    __shared__ __attribute__((aligned(16))) char sdO[AT_TILE_BYTES];
-    __shared__ float sL[AT_T], sD[AT_T];
-    const int b = blockIdx.z, h = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int STAGE = 2 * AT_TILE_BYTES + 4 * AT_T * 4;
+    __shared__ __attribute__((aligned(16))) char ring[AR_NS * STAGE];
+    const AttnBlock blk = attn_block();
+    const int b = blk.b, h = blk.h;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i16 = lane & 15, g = lane >> 4;
-    const int kblk = blockIdx.x * AT_T;
+    const int kblk = blk.x * AT_T;
     const int key = kblk + wave * 16 + i16;  // this lane's key (MFMA n index)
     const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
     const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
     const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
-    const float* lse = a.lse + ((size_t)b * a.H + h) * a.Sq;
+    const float* rowv = ((wave & 1) ? a.delta : a.lse) + ((size_t)b * a.H + h) * a.Sq;
+    const float c = a.scale * AT_LOG2E;
 
     // Kᵀ / Vᵀ as B operands: lane l needs K[key][32ks + 8g + j]
     bf16x8 kf[2], vf[2];
@@ -248,6 +428,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     kf[1] = load_frag_global(Kb, a.ldk, key, a.Sk, 32 + 8 * g);
     vf[0] = load_frag_global(Vb, a.ldv, key, a.Sk, 8 * g);
     vf[1] = load_frag_global(Vb, a.ldv, key, a.Sk, 32 + 8 * g);
+    vm_ready(kf[0]); vm_ready(kf[1]); vm_ready(vf[0]); vm_ready(vf[1]);
 
     f32x4 dk[4], dv[4];
 #pragma unroll
@@ -255,66 +436,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
         dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
         dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int nqt = (a.Sq + AT_T - 1) / AT_T;
     const int qt0 = CAUSAL ? kblk / AT_T : 0;
-    for (int qt = qt0; qt < nqt; ++qt) {
-        const int q0 = qt * AT_T;
-        __syncthreads();
-        stage_tile(sQ, Qb, a.ldq, q0, a.Sq, 0);
-        stage_tile(sdO, dOb, a.lddo, q0, a.Sq, 0);
-        {   // delta[q] = Σ_d dO[q,d]·O[q,d] for the tile's 64 queries: 4 threads per query row
-            const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
-            const int qq = q0 + ql;
-            float dsum = 0.f;
-            if (qq < a.Sq) {
-                const __bf16* od = a.o + ((size_t)b * a.Sq + qq) * a.ldo + h * AT_D + part * 16;
-                const __bf16* dd = dOb + (size_t)qq * a.lddo + part * 16;
-#pragma unroll
-                for (int c = 0; c < 16; c += 8) {
-                    bf16x8 x = *reinterpret_cast<const bf16x8*>(dd + c);
-                    bf16x8 y = *reinterpret_cast<const bf16x8*>(od + c);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) dsum += bf2f(x[j]) * bf2f(y[j]);
-                }
-            }
-            dsum += __shfl_xor(dsum, 1, 64);
-            dsum += __shfl_xor(dsum, 2, 64);
-            if (part == 0) {
-                sL[ql] = qq < a.Sq ? lse[qq] : 0.f;
-                sD[ql] = dsum;
-            }
-        }
-        __syncthreads();
-        f32x4 p[4], ds[4];
-#pragma unroll
-        for (int qb = 0; qb < 4; ++qb) {
-            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-            s = MFMA16(row_frag(sQ, qb * 16, 0), kf[0], s);
-            s = MFMA16(row_frag(sQ, qb * 16, 1), kf[1], s);
-            f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
-            dp = MFMA16(row_frag(sdO, qb * 16, 0), vf[0], dp);
-            dp = MFMA16(row_frag(sdO, qb * 16, 1), vf[1], dp);
-            // element r: query q0 + qb*16 + 4g + r, key `key`
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int ql = qb * 16 + 4 * g + r;
-                int qq = q0 + ql;
-                bool masked = qq >= a.Sq || key >= a.Sk || (CAUSAL && key > qq);
-                float pv = masked ? 0.f : __expf(s[r] * a.scale - sL[ql]);
-                p[qb][r] = pv;
-                ds[qb][r] = pv * (dp[r] - sD[ql]);
-            }
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            bf16x8 pb = pack_p(p[2 * half], p[2 * half + 1]);
-            bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                dv[d] = MFMA16(tr_frag(sdO, 32 * half, d * 16), pb, dv[d]);
-                dk[d] = MFMA16(tr_frag(sQ, 32 * half, d * 16), sb, dk[d]);
-            }
-        }
+    const int n = (a.Sq + AT_T - 1) / AT_T - qt0;  // query tiles of this workgroup
+    auto issue = [&](int i) {
+        char* st = ring + (i % AR_NS) * STAGE;
+        const int q0 = (qt0 + i) * AT_T;
+        AttnTile::issue(st, Qb, a.ldq, q0, a.Sq, 0, wave);
+        AttnTile::issue(st + AT_TILE_BYTES, dOb, a.lddo, q0, a.Sq, 0, wave);
+        glds4(rowv + min(q0 + lane, a.Sq - 1),
+              __builtin_amdgcn_readfirstlane(lds_addr_of(st + 2 * AT_TILE_BYTES + wave * AT_T * 4)));
+    };
+    for (int s = 0; s < AR_NS - 1 && s < n; ++s) issue(s);
+    for (int i = 0; i < n; ++i) {
+        ring_sync<5>(min(AR_NS - 2, n - 1 - i));
+        if (i + AR_NS - 1 < n) issue(i + AR_NS - 1);
+        const char* sQ = ring + (i % AR_NS) * STAGE;
+        const char* sdO = sQ + AT_TILE_BYTES;
+        const float* sL = reinterpret_cast<const float*>(sQ + 2 * AT_TILE_BYTES);
+        const float* sD = sL + AT_T;
+        dkv_step<CAUSAL>(sQ, sdO, sL, sD, (qt0 + i) * AT_T, key, kblk + wave * 16, a.Sq, a.Sk, c, kf, vf, dk, dv,
+                         nullptr, 0);
     }
     if (key < a.Sk) {
         size_t tok = (size_t)b * a.Sk + key;
@@ -332,15 +473,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     }
 }
 
-// dQ: workgroup = 64 queries, each wave 16 queries; loop over key tiles.
+// dQ: workgroup = 64 queries, each wave 16 queries; loop over key tiles (K, V through the ring).
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char sK[AT_TILE_BYTES];
-    __shared__ __attribute__((aligned(16))) char sV[AT_TILE_BYTES];
-    const int b = blockIdx.z, h = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char ring[AR_NS * 2 * AT_TILE_BYTES];
+    const AttnBlock blk = attn_block();
+    const int b = blk.b, h = blk.h;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i16 = lane & 15, g = lane >> 4;
-    const int qblk = blockIdx.x * AT_T;
+    const int qblk = (CAUSAL ? gridDim.x - 1 - blk.x : blk.x) * AT_T;
     const int q = qblk + wave * 16 + i16;
     const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
     const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
@@ -348,26 +489,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
     const size_t sidx = ((size_t)b * a.H + h) * a.Sq + q;
     const float lq = q < a.Sq ? a.lse[sidx] : 0.f;
-    float dq_delta = 0.f;  // Σ_d dO[q,d]·O[q,d]: the 4 lane groups sharing query q each sum 16 dims
-    if (q < a.Sq) {
-        const __bf16* od = a.o + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D + g * 16;
-        const __bf16* dd = dOb + (size_t)q * a.lddo + g * 16;
-#pragma unroll
-        for (int c = 0; c < 16; c += 8) {
-            bf16x8 x = *reinterpret_cast<const bf16x8*>(dd + c);
-            bf16x8 y = *reinterpret_cast<const bf16x8*>(od + c);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) dq_delta += bf2f(x[j]) * bf2f(y[j]);
-        }
-    }
-    dq_delta += __shfl_xor(dq_delta, 16, 64);
-    dq_delta += __shfl_xor(dq_delta, 32, 64);
+    const float dq_delta = q < a.Sq ? a.delta[sidx] : 0.f;
+    const float c = a.scale * AT_LOG2E, lq2 = lq * AT_LOG2E;
 
     bf16x8 qf[2], dof[2];
     qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
     qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
     dof[0] = load_frag_global(dOb, a.lddo, q, a.Sq, 8 * g);
     dof[1] = load_frag_global(dOb, a.lddo, q, a.Sq, 32 + 8 * g);
+    vm_ready(qf[0]); vm_ready(qf[1]); vm_ready(dof[0]); vm_ready(dof[1]);
+    vm_ready(lq); vm_ready(dq_delta);
 
     f32x4 dq[4];
 #pragma unroll
@@ -377,35 +508,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         int qlast = min(a.Sq, qblk + AT_T) - 1;
         nkt = min(nkt, qlast / AT_T + 1);
     }
+    auto issue = [&](int kt) {
+        char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
+        AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
+    };
+    for (int s = 0; s < AR_NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
+        ring_sync<4>(min(AR_NS - 2, nkt - 1 - kt));
+        if (kt + AR_NS - 1 < nkt) issue(kt + AR_NS - 1);
+        const char* sK = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        const char* sV = sK + AT_TILE_BYTES;
         const int key0 = kt * AT_T;
-        __syncthreads();
-        stage_tile(sK, Kb, a.ldk, key0, a.Sk, 0);
-        stage_tile(sV, Vb, a.ldv, key0, a.Sk, 0);
-        __syncthreads();
-        f32x4 ds[4];
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-            s = MFMA16(row_frag(sK, kb * 16, 0), qf[0], s);
-            s = MFMA16(row_frag(sK, kb * 16, 1), qf[1], s);
-            f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
-            dp = MFMA16(row_frag(sV, kb * 16, 0), dof[0], dp);
-            dp = MFMA16(row_frag(sV, kb * 16, 1), dof[1], dp);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int key = key0 + kb * 16 + 4 * g + r;
-                bool masked = key >= a.Sk || q >= a.Sq || (CAUSAL && key > q);
-                float pv = masked ? 0.f : __expf(s[r] * a.scale - lq);
-                ds[kb][r] = pv * (dp[r] - dq_delta);
-            }
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) dq[d] = MFMA16(tr_frag(sK, 32 * half, d * 16), sb, dq[d]);
-        }
+        if (tile_masked<CAUSAL>(key0, a.Sk, qblk + wave * 16) || qblk + wave * 16 + 16 > a.Sq)
+            dq_tile<CAUSAL, true>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq);
+        else
+            dq_tile<CAUSAL, false>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq);
     }
     if (q < a.Sq) {
         __bf16* out = a.dq + ((size_t)b * a.Sq + q) * a.lddq + h * AT_D;
@@ -479,9 +597,10 @@ __global__ __launch_bounds__(512) void attn_fwd_short_kernel(AttnArgs a) {
     float m = -INFINITY, l = 0.f;
     int nkt = (a.Sk + AT_T - 1) / AT_T;
     if (CAUSAL) nkt = min(nkt, (wave * 16 + 15) / AT_T + 1);
+    const float c = a.scale * AT_LOG2E;
     for (int kt = 0; kt < nkt; ++kt)
-        fwd_kv_tile<CAUSAL>(sK + kt * AT_TILE_BYTES, sV + kt * AT_TILE_BYTES, kt * AT_T, q, a.Sk, a.scale, qf, o, m,
-                            l);
+        fwd_tile<CAUSAL>(sK + kt * AT_TILE_BYTES, sV + kt * AT_TILE_BYTES, kt * AT_T, q, wave * 16, a.Sk, c, qf, o, m,
+                         l);
     fwd_store(a, b, h, q, o, m, l);
 }
 
@@ -541,6 +660,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     __syncthreads();
 
     // ---- phase 1: this wave's 16 keys
+    const float c = a.scale * AT_LOG2E;
     {
         const int key = wave * 16 + i16;
         const int kt = wave >> 2;                      // key tile of this wave
@@ -561,40 +681,8 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
             const char* tQ = sQ + qt * AT_TILE_BYTES;
             const char* tdO = sdO + qt * AT_TILE_BYTES;
             char* tS = sdS + (kt * AS_TILES + qt) * AT_TILE_BYTES;
-            f32x4 p[4], ds[4];
-#pragma unroll
-            for (int qb = 0; qb < 4; ++qb) {
-                f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-                s = MFMA16(row_frag(tQ, qb * 16, 0), kf[0], s);
-                s = MFMA16(row_frag(tQ, qb * 16, 1), kf[1], s);
-                f32x4 dp = f32x4{0.f, 0.f, 0.f, 0.f};
-                dp = MFMA16(row_frag(tdO, qb * 16, 0), vf[0], dp);
-                dp = MFMA16(row_frag(tdO, qb * 16, 1), vf[1], dp);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ql = qt * AT_T + qb * 16 + 4 * g + r;
-                    const bool masked = ql >= a.Sq || key >= a.Sk || (CAUSAL && key > ql);
-                    const float pv = masked ? 0.f : __expf(s[r] * a.scale - sL[ql]);
-                    p[qb][r] = pv;
-                    ds[qb][r] = pv * (dp[r] - sD[ql]);
-                }
-                // dS[key][q..q+3] -> key-major LDS tile (one 8-byte store per lane)
-                bf16x4 w;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) w[r] = f2bf(ds[qb][r]);
-                const int qc = qb * 16 + 4 * g;      // query column inside the tile
-                *reinterpret_cast<bf16x4*>(tS + tile_off(krow, qc >> 3) + (qc & 7) * 2) = w;
-            }
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                bf16x8 pb = pack_p(p[2 * half], p[2 * half + 1]);
-                bf16x8 sb = pack_p(ds[2 * half], ds[2 * half + 1]);
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    dv[d] = MFMA16(tr_frag(tdO, 32 * half, d * 16), pb, dv[d]);
-                    dk[d] = MFMA16(tr_frag(tQ, 32 * half, d * 16), sb, dk[d]);
-                }
-            }
+            dkv_step<CAUSAL>(tQ, tdO, sL + qt * AT_T, sD + qt * AT_T, qt * AT_T, key, wave * 16, a.Sq, a.Sk, c, kf, vf,
+                             dk, dv, tS, krow);
         }
         if (key < a.Sk) {
             size_t tok = (size_t)b * a.Sk + key;
@@ -728,6 +816,7 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
         return check_launch("attn_bwd");
     }
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
+    hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(B * Sq * H * 4, 256)), dim3(256), 0, s, a);
     if (causal) {
         hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, gk, dim3(256), 0, s, a);
         hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, gq, dim3(256), 0, s, a);

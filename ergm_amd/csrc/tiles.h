@@ -129,6 +129,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
                  : "memory");
 }
 
+// 4-B-per-lane LDS-DMA: LDS[lds_addr + 4*lane] = *gsrc (a 256-B row of floats per wave-instruction).
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
