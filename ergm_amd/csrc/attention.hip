@@ -90,6 +90,23 @@ struct AttnArgs {
 
 constexpr float AT_LOG2E = 1.4426950408889634f;
 
+// All-reduce over the 4 16-lane rows of a wave (lanes l, l^16, l^32, l^48) with the gfx950 row swaps
+// (v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip as ds_bpermute would take).  Each
+// swap of x with itself yields (x of the even row, x of the odd row) in every lane, so every lane
+// combines the same two values in the same order.
+__device__ __forceinline__ float rows_max(float x) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float rows_sum(float x) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // exp(scale·s − shift) given c = scale·log2e and shift2 = shift·log2e.
 __device__ __forceinline__ float exp_sc(float s, float c, float shift2) {
     return __builtin_amdgcn_exp2f(fmaf(s, c, -shift2));
@@ -125,8 +142,7 @@ __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int 
             }
             mx = fmaxf(mx, x);
         }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = rows_max(mx);
     const float mnew = fmaxf(m, mx);
     const float m2 = (mnew == -INFINITY ? 0.f : mnew) * c;
     const float alpha = exp_sc(m, c, m2);
@@ -139,8 +155,7 @@ __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int 
             s[kb][r] = p;
             rs += p;
         }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = rows_sum(rs);
     l = l * alpha + rs;
     m = mnew;
 #pragma unroll
@@ -309,7 +324,6 @@ __device__ __forceinline__ AttnBlock attn_block() {
     return r;
 }
 
-constexpr int AR_NS = 3;                       // LDS ring stages of the tiled kernels
 using AttnTile = GldsTile<AT_T, false, 4>;      // one 64x64 bf16 tile: 2 LDS-DMA wave-instructions per wave
 
 // Make the compiler wait for a register operand loaded before the ring prologue: its own vmcnt wait then
@@ -322,16 +336,16 @@ __device__ __forceinline__ void vm_ready(float x) { asm volatile("" ::"v"(x)); }
 
 // Ring step: wait until this wave's DMA for the current stage landed (`after` younger stages may stay in
 // flight), finish this wave's LDS reads of the slot about to be refilled, then one workgroup barrier.
-template <int LPS>
+template <int LPS, int NS>
 __device__ __forceinline__ void ring_sync(int after) {
-    wait_stages<LPS, AR_NS - 2>(after);
+    wait_stages<LPS, NS - 2>(after);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 }
 
-template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char ring[AR_NS * 2 * AT_TILE_BYTES];  // [stage][K|V]
+template <bool CAUSAL, int NS>
+__global__ __launch_bounds__(256, 4) void attn_fwd_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) char ring[NS * 2 * AT_TILE_BYTES];  // [stage][K|V]
     const AttnBlock blk = attn_block();
     const int b = blk.b, h = blk.h;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -361,15 +375,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         nkt = min(nkt, qlast / AT_T + 1);
     }
     auto issue = [&](int kt) {
-        char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
         AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
     };
-    for (int s = 0; s < AR_NS - 1 && s < nkt; ++s) issue(s);
+    for (int s = 0; s < NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
-        ring_sync<4>(min(AR_NS - 2, nkt - 1 - kt));
-        if (kt + AR_NS - 1 < nkt) issue(kt + AR_NS - 1);
-        const char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        ring_sync<4, NS>(min(NS - 2, nkt - 1 - kt));
+        if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+        const char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         fwd_tile<CAUSAL>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l);
     }
     fwd_store(a, b, h, q, o, m, l);
@@ -405,10 +419,10 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
 
 // dK, dV: workgroup = 64 keys of one (b, h), each wave 16 keys; loop over query tiles.  A ring stage holds
 // the Q and dO tiles and the tile's 64 LSE and δ values (one 256-B DMA per wave: waves 0/2 LSE, 1/3 δ).
-template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
+template <bool CAUSAL, int NS>
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkv_kernel(AttnArgs a) {
     constexpr int STAGE = 2 * AT_TILE_BYTES + 4 * AT_T * 4;
-    __shared__ __attribute__((aligned(16))) char ring[AR_NS * STAGE];
+    __shared__ __attribute__((aligned(16))) char ring[NS * STAGE];
     const AttnBlock blk = attn_block();
     const int b = blk.b, h = blk.h;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -439,18 +453,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     const int qt0 = CAUSAL ? kblk / AT_T : 0;
     const int n = (a.Sq + AT_T - 1) / AT_T - qt0;  // query tiles of this workgroup
     auto issue = [&](int i) {
-        char* st = ring + (i % AR_NS) * STAGE;
+        char* st = ring + (i % NS) * STAGE;
         const int q0 = (qt0 + i) * AT_T;
         AttnTile::issue(st, Qb, a.ldq, q0, a.Sq, 0, wave);
         AttnTile::issue(st + AT_TILE_BYTES, dOb, a.lddo, q0, a.Sq, 0, wave);
         glds4(rowv + min(q0 + lane, a.Sq - 1),
               __builtin_amdgcn_readfirstlane(lds_addr_of(st + 2 * AT_TILE_BYTES + wave * AT_T * 4)));
     };
-    for (int s = 0; s < AR_NS - 1 && s < n; ++s) issue(s);
+    for (int s = 0; s < NS - 1 && s < n; ++s) issue(s);
     for (int i = 0; i < n; ++i) {
-        ring_sync<5>(min(AR_NS - 2, n - 1 - i));
-        if (i + AR_NS - 1 < n) issue(i + AR_NS - 1);
-        const char* sQ = ring + (i % AR_NS) * STAGE;
+        ring_sync<5, NS>(min(NS - 2, n - 1 - i));
+        if (i + NS - 1 < n) issue(i + NS - 1);
+        const char* sQ = ring + (i % NS) * STAGE;
         const char* sdO = sQ + AT_TILE_BYTES;
         const float* sL = reinterpret_cast<const float*>(sQ + 2 * AT_TILE_BYTES);
         const float* sD = sL + AT_T;
@@ -474,9 +488,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
 }
 
 // dQ: workgroup = 64 queries, each wave 16 queries; loop over key tiles (K, V through the ring).
-template <bool CAUSAL>
+template <bool CAUSAL, int NS>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char ring[AR_NS * 2 * AT_TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char ring[NS * 2 * AT_TILE_BYTES];
     const AttnBlock blk = attn_block();
     const int b = blk.b, h = blk.h;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -509,15 +523,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         nkt = min(nkt, qlast / AT_T + 1);
     }
     auto issue = [&](int kt) {
-        char* st = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
         AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
     };
-    for (int s = 0; s < AR_NS - 1 && s < nkt; ++s) issue(s);
+    for (int s = 0; s < NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
-        ring_sync<4>(min(AR_NS - 2, nkt - 1 - kt));
-        if (kt + AR_NS - 1 < nkt) issue(kt + AR_NS - 1);
-        const char* sK = ring + (kt % AR_NS) * 2 * AT_TILE_BYTES;
+        ring_sync<4, NS>(min(NS - 2, nkt - 1 - kt));
+        if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+        const char* sK = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         const char* sV = sK + AT_TILE_BYTES;
         const int key0 = kt * AT_T;
         if (tile_masked<CAUSAL>(key0, a.Sk, qblk + wave * 16) || qblk + wave * 16 + 16 > a.Sq)
@@ -751,10 +765,37 @@ using namespace ergm;
 
 namespace {
 bool g_attn_generic = false;  // ergm_attn_tune: force the tiled kernels even for short sequences
+int g_attn_ns = 0;            // ergm_attn_tune: ring stages of the tiled kernels (0: per-kernel defaults)
+
+template <bool CAUSAL, int NS>
+void launch_tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
+    hipLaunchKernelGGL((attn_fwd_kernel<CAUSAL, NS>), grid, dim3(256), 0, s, a);
+}
+// Defaults measured with tools/attn_bench.py at the C4 shape (S = 512): forward and dK/dV 2 stages (the
+// dK/dV kernel then fits 3 waves per SIMD without spills), dQ 3.
+template <bool CAUSAL>
+void tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
+    if (g_attn_ns == 3) launch_tiled_fwd<CAUSAL, 3>(grid, s, a);
+    else if (g_attn_ns == 4) launch_tiled_fwd<CAUSAL, 4>(grid, s, a);
+    else launch_tiled_fwd<CAUSAL, 2>(grid, s, a);
+}
+template <bool CAUSAL>
+void tiled_bwd(dim3 gk, dim3 gq, hipStream_t s, const AttnArgs& a) {
+    const int ns_kv = g_attn_ns ? g_attn_ns : 2, ns_q = g_attn_ns ? g_attn_ns : 3;
+    if (ns_kv == 3) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 3>), gk, dim3(256), 0, s, a);
+    else if (ns_kv == 4) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 4>), gk, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 2>), gk, dim3(256), 0, s, a);
+    if (ns_q == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 2>), gq, dim3(256), 0, s, a);
+    else if (ns_q == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 4>), gq, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 3>), gq, dim3(256), 0, s, a);
+}
 }
 
 extern "C" int ergm_attn_tune(int force_generic) {
-    g_attn_generic = force_generic != 0;
+    const int ns = (force_generic >> 4) & 15;
+    ERGM_CHECK_ARG(ns == 0 || ns == 2 || ns == 3 || ns == 4, "attn_tune: ring stages must be 2, 3 or 4");
+    g_attn_generic = (force_generic & 1) != 0;
+    g_attn_ns = ns;
     return ERGM_OK;
 }
 
@@ -776,8 +817,8 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
         return check_launch("attn_fwd");
     }
     dim3 grid(cdiv(Sq, AT_T), H, B);
-    if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, a);
+    if (causal) tiled_fwd<true>(grid, s, a);
+    else tiled_fwd<false>(grid, s, a);
     return check_launch("attn_fwd");
 }
 
@@ -817,12 +858,7 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
     }
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
     hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(B * Sq * H * 4, 256)), dim3(256), 0, s, a);
-    if (causal) {
-        hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, gk, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, gq, dim3(256), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(attn_bwd_dkv_kernel<false>, gk, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, gq, dim3(256), 0, s, a);
-    }
+    if (causal) tiled_bwd<true>(gk, gq, s, a);
+    else tiled_bwd<false>(gk, gq, s, a);
     return check_launch("attn_bwd");
 }

@@ -1,7 +1,7 @@
 """Isolated attention timings at the training configs' shapes (HIP-graph replay, no concurrency), with
 algorithmic TFLOP/s: forward 4·B·H·Sq·Sk·64 FLOP (half of it for causal), backward 2.5x the forward
 (dV, dP, dS·K for dQ, dSᵀ·Q for dK; the recomputed QKᵀ not counted).  Usage (GPU box):
-python tools/attn_bench.py [--generic]"""
+python tools/attn_bench.py [--generic] [--ns 2,3,4] [--only c4]"""
 import os
 import sys
 
@@ -36,11 +36,20 @@ def timed(fn):
 
 
 def main():
-    dev = torch.device("cuda:0")
     lib = L.load()
-    if "--generic" in sys.argv:
-        lib.ergm_attn_tune(1)
+    arg = lambda k, d: sys.argv[sys.argv.index(k) + 1] if k in sys.argv else d  # noqa: E731
+    for ns in [int(x) for x in arg("--ns", "0").split(",")]:
+        L.check(lib.ergm_attn_tune(int("--generic" in sys.argv) | (ns << 4)), "attn_tune")
+        if ns:
+            print(f"ring stages {ns}")
+        run(arg("--only", None))
+
+
+def run(only):
+    dev = torch.device("cuda:0")
     for name, (B, S, H) in SHAPES.items():
+        if only and name != only:
+            continue
         E = 64 * H
         T = B * S
         for causal in (True, False):
