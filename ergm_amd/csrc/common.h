@@ -60,17 +60,28 @@ struct WqJobs {
     int n;
 };
 
-// wave-level reductions over 64 lanes
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// wave-level reductions over 64 lanes, all VALU (no ds_bpermute round trips): DPP quad_perm [1,0,3,2]
+// and [2,3,0,1], row_half_mirror and row_mirror inside each 16-lane row, then the gfx950 row swaps
+// v_permlane16_swap / v_permlane32_swap across rows.  Every step combines a lane's value with its
+// partner's by a commutative op, so all 64 lanes end with the bit-identical result.  Full waves only.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce(float v) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+    v = op(v, dpp_f32<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp_f32<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp_f32<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_f32<0x140>(v));  // row_mirror
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+__device__ __forceinline__ float wave_sum(float v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v); }
 
 // gelu_new (transformers NewGELUActivation): 0.5x(1+tanh(sqrt(2/pi)(x+0.044715x^3)))
 __device__ __forceinline__ float gelu_new(float x) {

@@ -70,9 +70,6 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const void* __restrict_
 }
 
 // ---- weights: batched over the matrices of one block (WqJobs in common.h) ------------------------
-__device__ __forceinline__ float load_w(const WqJob& j, size_t idx) {
-    return j.w_bf16 ? bf2f(reinterpret_cast<const __bf16*>(j.W)[idx]) : reinterpret_cast<const float*>(j.W)[idx];
-}
 
 __device__ __forceinline__ int find_job(const WqJobs& J, int bid, bool q) {
     int k = 0;
@@ -82,28 +79,46 @@ __device__ __forceinline__ int find_job(const WqJobs& J, int bid, bool q) {
     return k;
 }
 
-// block = (job, 64-column tile, 256-row chunk): column amax, merged with atomicMax on the bit pattern
-// (non-negative floats order like their bits: the result is exact and order-independent)
+constexpr int WQ_AMAX_COLS = 512;  // columns per amax block: 8 per lane (one 16-B bf16 load per row)
+constexpr int WQ_AMAX_ROWS = 128;  // rows per amax block
+
+// block = (job, 512-column tile, 128-row chunk): each lane keeps the running |w| max of 8 consecutive
+// columns over every 4th row of the chunk; the 4 waves are merged through LDS and the result merged
+// across chunks with atomicMax on the bit pattern (non-negative floats order like their bits: exact and
+// order-independent)
 __global__ __launch_bounds__(256) void wq_amax_kernel(WqJobs J) {
-    __shared__ float red[4][64];
+    __shared__ float red[4][WQ_AMAX_COLS];
     const int ji = find_job(J, blockIdx.x, false);
     const WqJob& jb = J.j[ji];
     const int local = blockIdx.x - jb.blk_amax;
-    const int nt = jb.N / 64, kc = local / nt, n0 = (local % nt) * 64;
-    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int k0 = kc * 256, k1 = min(jb.K, k0 + 256);
-    float m = 0.f;
-    for (int k = k0 + rg; k < k1; k += 4) m = fmaxf(m, fabsf(load_w(jb, (size_t)k * jb.ldw + n0 + col)));
-    red[rg][col] = m;
+    const int nt = (jb.N + WQ_AMAX_COLS - 1) / WQ_AMAX_COLS, kc = local / nt, n0 = (local % nt) * WQ_AMAX_COLS;
+    const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int c = n0 + lane * 8;
+    const int k0 = kc * WQ_AMAX_ROWS, k1 = min(jb.K, k0 + WQ_AMAX_ROWS);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = 0.f;
+    if (c < jb.N) {
+#pragma unroll 4
+        for (int k = k0 + rg; k < k1; k += 4) {
+            float v[8];
+            load8(jb.W, jb.w_bf16, (size_t)k * jb.ldw + c, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(v[j]));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rg][lane * 8 + j] = m[j];
     __syncthreads();
-    if (rg == 0) {
-        m = fmaxf(fmaxf(red[0][col], red[1][col]), fmaxf(red[2][col], red[3][col]));
-        atomicMax(jb.amax + n0 + col, __float_as_uint(m));
+    for (int i = threadIdx.x; i < WQ_AMAX_COLS; i += 256) {
+        const float r = fmaxf(fmaxf(red[0][i], red[1][i]), fmaxf(red[2][i], red[3][i]));
+        if (n0 + i < jb.N) atomicMax(jb.amax + n0 + i, __float_as_uint(r));
     }
 }
 
-// block = (job, 64-column tile, 64-row tile): quantise with the column scale, transpose through LDS,
-// write 64 rows of Wt (one per column) x 64 bytes
+// block = (job, 64-column tile, 64-row tile): thread = 4 consecutive rows x 4 consecutive columns
+// (8-B bf16 / 16-B f32 loads), quantised with the column scales and packed per column into one dword
+// of 4 k-consecutive bytes, transposed through LDS; then 64 rows of Wt (one per column) x 64 bytes
 __global__ __launch_bounds__(256) void wq_quant_kernel(WqJobs J) {
     constexpr int LD = 80;  // bytes per LDS row (16-B aligned reads)
     __shared__ __attribute__((aligned(16))) uint8_t tile[64 * LD];
@@ -111,23 +126,43 @@ __global__ __launch_bounds__(256) void wq_quant_kernel(WqJobs J) {
     const WqJob& jb = J.j[ji];
     const int local = blockIdx.x - jb.blk_q;
     const int nt = jb.N / 64, kt = local / nt, n0 = (local % nt) * 64, k0 = kt * 64;
-    const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const float amax = __uint_as_float(jb.amax[n0 + col]);
-    const float s = amax > 0.f ? amax / 448.f : 1.f;
-    if (kt == 0 && rg == 0) jb.scale[n0 + col] = s;
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int kk = rg * 16 + i, k = k0 + kk;
-        const float w = k < jb.K ? load_w(jb, (size_t)k * jb.ldw + n0 + col) : 0.f;
-        tile[col * LD + kk] = fp8x1(w / s);
+    const int nq = (threadIdx.x & 15) * 4, kq = (threadIdx.x >> 4) * 4;
+    float s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float amax = __uint_as_float(jb.amax[n0 + nq + j]);
+        s[j] = amax > 0.f ? amax / 448.f : 1.f;
     }
+    if (kt == 0 && kq == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) jb.scale[n0 + nq + j] = s[j];
+    }
+    float w[4][4];  // [row][column]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int k = k0 + kq + r;
+        const size_t idx = (size_t)k * jb.ldw + n0 + nq;
+        if (k >= jb.K) {
+            w[r][0] = w[r][1] = w[r][2] = w[r][3] = 0.f;
+        } else if (jb.w_bf16) {
+            const bf16x4 x = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(jb.W) + idx);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[r][j] = bf2f(x[j]);
+        } else {
+            const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(jb.W) + idx);
+            w[r][0] = x.x; w[r][1] = x.y; w[r][2] = x.z; w[r][3] = x.w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<uint32_t*>(tile + (nq + j) * LD + kq) =
+            fp8x4(w[0][j] / s[j], w[1][j] / s[j], w[2][j] / s[j], w[3][j] / s[j]);
     __syncthreads();
     const int n = threadIdx.x >> 2, q = threadIdx.x & 3;
     if (k0 + q * 16 < jb.K)
         *reinterpret_cast<uint4*>(jb.Wt + (size_t)(n0 + n) * jb.ldt + k0 + q * 16) =
             *reinterpret_cast<const uint4*>(tile + n * LD + q * 16);
 }
-
 int quant_weights_fp8(const WqJobs& J0, hipStream_t s) {
     WqJobs J = J0;
     ERGM_CHECK_ARG(J.n >= 1 && J.n <= 8, "quant_weights_fp8: 1..8 matrices per launch");
@@ -135,11 +170,11 @@ int quant_weights_fp8(const WqJobs& J0, hipStream_t s) {
     for (int i = 0; i < J.n; ++i) {
         WqJob& j = J.j[i];
         ERGM_CHECK_ARG(j.W && j.Wt && j.scale && j.amax && j.N % 64 == 0 && j.K % 64 == 0 && j.ldt >= j.K &&
-                           j.ldt % 16 == 0 && j.ldw >= j.N,
+                           j.ldt % 16 == 0 && j.ldw >= j.N && j.ldw % 8 == 0,
                        "quant_weights_fp8: bad matrix %d (K=%d N=%d)", i, j.K, j.N);
         j.blk_amax = ba;
         j.blk_q = bq;
-        ba += (j.N / 64) * cdiv(j.K, 256);
+        ba += cdiv(j.N, WQ_AMAX_COLS) * cdiv(j.K, WQ_AMAX_ROWS);
         bq += (j.N / 64) * (j.K / 64);
     }
     hipLaunchKernelGGL(wq_amax_kernel, dim3(ba), dim3(256), 0, s, J);
