@@ -172,6 +172,37 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
     }
 }
 
+// LDS-free epilogue for tiles computed with SWAPPED MFMA operands (mfma(B-frag, A-frag) = Cᵀ fragments:
+// lane (g = l>>4, i = l&15) holds C[m = 16·blk + i][n = 16·j + 4g + r], r = 0..3, i.e. 4 consecutive
+// columns of one row).  v_permlane16_swap of fragments (i, i+1) exchanges the odd 16-lane rows of the
+// first with the even rows of the second, after which every lane holds 8 consecutive columns of one row
+// (block i + (g & 1), columns 16j + 8(g >> 1) ..+7): one 8-wide epilogue store per fragment pair, no LDS
+// staging and no barriers.
+template <int WGN, int EPI, bool OUT_BF16, int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void store_tile_direct(const GemmArgs& a, f32x4 (&acc)[FM][FN], int m0, int n0,
+                                                  float alpha) {
+    static_assert(FM % 2 == 0, "direct store pairs row fragments");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave / WGN, wn = wave % WGN;
+    const int g = lane >> 4, i16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < FM; i += 2)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            float v[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]),
+                                                           __float_as_uint(acc[i + 1][j][r]), false, false);
+                v[r] = __uint_as_float(sw[0]) * alpha;
+                v[4 + r] = __uint_as_float(sw[1]) * alpha;
+            }
+            const int m = m0 + wm * WM + (i + (g & 1)) * 16 + i16;
+            const int n = n0 + wn * WN + j * 16 + 8 * (g >> 1);
+            if (m < a.M && n < a.N) epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
+        }
+}
+
 // bijective XCD-grouping remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous range.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int NX = 8;
@@ -270,7 +301,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // Pipelined variant: NS-stage LDS ring filled by LDS-DMA (GldsTile, tiles.h), counted waits, raw barrier.
-template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     constexpr int NW = WGM * WGN;
     constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -329,14 +360,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < FN; ++j) {
+                    if constexpr (DIRECT)  // Cᵀ fragments (store_tile_direct)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
         }
     }
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
-    float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
-    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
+    if constexpr (DIRECT) {
+        store_tile_direct<WGN, EPI, OUT_BF16, FM, FN, WM, WN>(a, acc, m0, n0, alpha);
+    } else {
+        float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
+        store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
+    }
 }
 
 // Warp-specialised variant: NP producer waves only issue the LDS-DMA fills, the WGM x WGN consumer
@@ -526,7 +565,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int spli
 // Pipelined-kernel configurations (tile BM x BN, wave grid WGM x WGN, LDS stages NS).
 struct PipeCfg {
     int bm, bn, wgm, wgn, ns;
-    int np = 0;  // > 0: warp-specialised kernel with np producer waves
+    int np = 0;      // > 0: warp-specialised kernel with np producer waves
+    bool direct = false;  // LDS-free epilogue (store_tile_direct); split-K partials keep the staged one
 };
 static constexpr PipeCfg kCfgs[] = {
     {64, 64, 2, 2, 4},     // 0
@@ -552,6 +592,10 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 5, 4},   // 19
     {128, 128, 2, 2, 4, 4},  // 20
     {128, 128, 4, 2, 4, 4},  // 21
+    // LDS-free epilogue variants
+    {256, 256, 4, 2, 2, 0, true},  // 22 the LM-head tile of cfg 6
+    {128, 128, 4, 2, 2, 0, true},  // 23 cfg 10
+    {128, 128, 2, 2, 2, 0, true},  // 24 cfg 2
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -711,7 +755,7 @@ static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
         k_full = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, EPI, OB>;
     } else {
         k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
-        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>;
+        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct>;
     }
     static bool attr = (hipFuncSetAttribute((const void*)k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         hipFuncSetAttribute((const void*)k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -745,7 +789,10 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 18: launch_pipe_cfg<18, AKM, BKN, EPI, OB>(a, split, s); break;
         case 19: launch_pipe_cfg<19, AKM, BKN, EPI, OB>(a, split, s); break;
         case 20: launch_pipe_cfg<20, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 21: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 22: launch_pipe_cfg<22, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 23: launch_pipe_cfg<23, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<24, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 

@@ -6,7 +6,10 @@ the distinct GEMM shapes (ergm_gemm_trace), and for each shape — largest first
 configurations through ergm_gemm_set_override, keeping one only if the measured step time drops by
 more than the noise threshold (and again on a confirming re-measurement).
 
-    python tools/step_tune.py [--config c2|c4|c5] [--steps 30] [--out gpurun_out/step_tune.json]
+    python tools/step_tune.py [--config c2|c4|c5] [--steps 30] [--splits 1,2,4] [--out gpurun_out/step_tune.json]
+
+Split-K candidates (--splits) use the plan's scratch for their slab; a split that does not fit is
+reported by the GEMM as an error and skipped.
 """
 from __future__ import annotations
 
@@ -23,10 +26,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from ergm_amd import _lib as L  # noqa: E402
 
-CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13]  # kCfgs indices (gemm.hip)
+CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13, 22, 23, 24]  # kCfgs indices (gemm.hip)
 TILE = {0: (64, 64), 1: (128, 128), 2: (128, 128), 3: (128, 128), 4: (256, 128), 6: (256, 256), 7: (128, 64),
         8: (64, 128), 9: (256, 128), 10: (128, 128), 11: (64, 64), 12: (128, 64), 13: (64, 128), 14: (128, 128),
-        15: (128, 128)}
+        15: (128, 128), 22: (256, 256), 23: (128, 128), 24: (128, 128)}
 
 
 def main():
@@ -35,6 +38,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--threshold", type=float, default=0.005)
     ap.add_argument("--max-shapes", type=int, default=24)
+    ap.add_argument("--splits", default="1")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     args = ap.parse_args()
     from ergm_amd.config import ERGMConfig
@@ -103,22 +107,22 @@ def main():
     for key in shapes:
         M, N, K, al, bl = key
         best = None  # None = the automatic choice
-        for c in CANDIDATES:
+        splits = [int(x) for x in args.splits.split(",")]
+        for c, sp in [(c, sp) for sp in splits for c in CANDIDATES]:
             bm, bn = TILE[c]
             tiles = -(-M // bm) * -(-N // bn)
-            if tiles < 24 or tiles > 20000:
+            if tiles < 24 or tiles > 20000 or (sp > 1 and (K // sp < 512 or tiles * sp > 2048)):
                 continue
-            # split 1 only: the plan's workspace was sized for the automatic choice
             try:
-                t_inc, t_cand = ab(key, best, (c, 1), rounds=1)
+                t_inc, t_cand = ab(key, best, (c, sp), rounds=1)
                 if t_cand < t_inc * (1.0 - args.threshold):
-                    t_inc, t_cand = ab(key, best, (c, 1), rounds=2)  # confirm
+                    t_inc, t_cand = ab(key, best, (c, sp), rounds=2)  # confirm
                     if t_cand < t_inc * (1.0 - args.threshold):
-                        print(f"  {M}x{N}x{K} al{al} bl{bl}: c{c} {t_cand:.3f} vs {t_inc:.3f} ms/step", flush=True)
-                        best = (c, 1)
+                        print(f"  {M}x{N}x{K} al{al} bl{bl}: c{c}s{sp} {t_cand:.3f} vs {t_inc:.3f} ms/step", flush=True)
+                        best = (c, sp)
                         set_cfg(key, best)
             except Exception as ex:  # noqa: BLE001  (a configuration the shape cannot take)
-                print(f"  {M}x{N}x{K} c{c}: {ex}", flush=True)
+                print(f"  {M}x{N}x{K} c{c}s{sp}: {ex}", flush=True)
                 set_cfg(key, best)
         if best is not None:
             chosen[key] = best
