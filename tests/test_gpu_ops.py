@@ -220,6 +220,34 @@ def test_attention_cross_strided(gpu):
     assert _rel(heads(o), ref) < 8e-3
 
 
+@pytest.mark.parametrize("B,H,Sq,Sk,causal", [(2, 3, 200, 333, False), (1, 2, 300, 300, True),
+                                              (2, 2, 520, 64, False), (8, 12, 512, 512, False)])
+def test_attention_tiled_ragged(gpu, B, H, Sq, Sk, causal):
+    """The LDS-DMA ring kernels (Sq or Sk > 128): ragged last tiles (rows clamped, keys masked), Sq != Sk,
+    K/V strided inside a wider projection buffer, the C4 cross shape; forward and backward vs fp32."""
+    E = 64 * H
+    torch.manual_seed(Sq * 3 + Sk + H)
+    q = torch.randn(B * Sq, E, device=gpu).bfloat16()
+    kv = torch.randn(B * Sk, 3 * E, device=gpu).bfloat16()  # K/V at column offsets E and 2E, ld = 3E
+    k, v = kv[:, E:2 * E], kv[:, 2 * E:]
+    o, lse = ops.attn_fwd(q, k, v, B, H, Sq, Sk, causal)
+
+    def heads(t, S):
+        return t.float().reshape(B, S, H, 64).permute(0, 2, 1, 3)
+    qf, kf, vf = heads(q, Sq).requires_grad_(True), heads(k, Sk).requires_grad_(True), heads(v, Sk).requires_grad_(True)
+    w = torch.matmul(qf, kf.transpose(-1, -2)) / 8.0
+    if causal:
+        w = w.masked_fill(~torch.tril(torch.ones(Sq, Sk, dtype=torch.bool, device=gpu)), float("-inf"))
+    ref = torch.softmax(w, -1) @ vf
+    assert _rel(heads(o, Sq), ref.detach()) < 8e-3
+    assert _rel(lse, torch.logsumexp(w, -1).detach()) < 1e-4
+    dout = torch.randn(B * Sq, E, device=gpu).bfloat16()
+    ref.backward(heads(dout, Sq))
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal)
+    for got, want, S in ((dq, qf.grad, Sq), (dk, kf.grad, Sk), (dv, vf.grad, Sk)):
+        assert _rel(heads(got, S), want) < 2e-2
+
+
 @pytest.mark.parametrize("rows,E", [(2048, 768), (100, 1024), (64, 64), (33, 128)])
 def test_layernorm(gpu, rows, E):
     torch.manual_seed(rows + E)
