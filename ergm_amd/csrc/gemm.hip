@@ -41,6 +41,7 @@ struct GemmArgs {
     float* slab;        // split-K partials [z][M][N] (f32) or nullptr
     const float* a_scale;  // fp8 GEMM: per-row dequantisation scale of A [M] (nullptr: none)
     const float* b_scale;  // fp8 GEMM: per-column dequantisation scale of B [N]
+    int nt_store;          // bf16 C written with non-temporal stores (streamed output)
 };
 
 template <int EPI, bool OUT_BF16>
@@ -102,7 +103,9 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.C) + idx) = o;
+        bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.C) + idx);
+        if (a.nt_store) __builtin_nontemporal_store(o, dst);
+        else *dst = o;
     } else {
         float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + idx);
         float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
@@ -1045,6 +1048,11 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     a.k_per_split = p.kps;
     a.slab = nullptr;
     a.a_scale = a.b_scale = nullptr;
+    // the vocabulary-wide bf16 logits (206 MB at C2) are streamed out with non-temporal stores so they
+    // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
+    // profiles/r01_overlap_experiments.txt #14); ERGM_NT_STORE=0 disables (A/B)
+    static const int nt_env = getenv("ERGM_NT_STORE") ? atoi(getenv("ERGM_NT_STORE")) : 1;
+    a.nt_store = nt_env && d->c_dtype == ERGM_BF16 && d->N >= 32768;
     hipStream_t s = as_stream(stream);
     if (p.split > 1) {
         size_t need = (size_t)p.split * d->M * d->N * sizeof(float);
