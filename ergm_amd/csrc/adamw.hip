@@ -8,6 +8,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ergm {
 
@@ -37,7 +38,24 @@ __device__ __forceinline__ float4 nt_load4(const float4* p) {  // gradients are 
     return make_float4(t[0], t[1], t[2], t[3]);
 }
 
+__device__ __forceinline__ void nt_store4(float4* p, const float4& x) {
+    __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<f32x4*>(p));
+}
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float4* p) {
+    if constexpr (NT) return nt_load4(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float4* p, const float4& x) {
+    if constexpr (NT) nt_store4(p, x);
+    else *p = x;
+}
+
 // Two float4 groups per thread per iteration (8 independent 16-B loads in flight before any math).
+// NT: parameters and moments are also streamed with non-temporal loads / stores (each is touched once
+// per step), so the pass does not evict the operands of the GEMMs it overlaps.
+template <bool NT>
 __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                     float4* __restrict__ m, float4* __restrict__ v,
                                                     bf16x4* __restrict__ pb, size_t n4, float decay, float one_m_b1,
@@ -47,25 +65,25 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, cons
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += 2 * stride) {
         const size_t i2 = i + stride;
         const bool two = i2 < n4;
-        float4 p0 = p[i], g0 = nt_load4(g + i), m0 = m[i], v0 = v[i];
+        float4 p0 = ld4<NT>(p + i), g0 = nt_load4(g + i), m0 = ld4<NT>(m + i), v0 = ld4<NT>(v + i);
         float4 p1, g1, m1, v1;
         if (two) {
-            p1 = p[i2];
+            p1 = ld4<NT>(p + i2);
             g1 = nt_load4(g + i2);
-            m1 = m[i2];
-            v1 = v[i2];
+            m1 = ld4<NT>(m + i2);
+            v1 = ld4<NT>(v + i2);
         }
         bf16x4 o0, o1;
         adamw_one(p0, g0, m0, v0, o0, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
-        p[i] = p0;
-        m[i] = m0;
-        v[i] = v0;
+        st4<NT>(p + i, p0);
+        st4<NT>(m + i, m0);
+        st4<NT>(v + i, v0);
         if (pb) pb[i] = o0;
         if (two) {
             adamw_one(p1, g1, m1, v1, o1, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
-            p[i2] = p1;
-            m[i2] = m1;
-            v[i2] = v1;
+            st4<NT>(p + i2, p1);
+            st4<NT>(m + i2, m1);
+            st4<NT>(v + i2, v1);
             if (pb) pb[i2] = o1;
         }
     }
@@ -143,9 +161,17 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     float one_m_b2 = (float)(1.0 - (double)beta2);
     unsigned grid = grid_for2(n4);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
-    hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
-                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2, one_m_b2, eps, step_size,
-                       bc2_sqrt);
+    // non-temporal parameter / moment traffic: C2 +1.2 %, C5 +0.6 % (profiles/r01_overlap_experiments.txt
+    // #15); ERGM_ADAMW_NT=0 disables (A/B)
+    static const bool nt = !getenv("ERGM_ADAMW_NT") || atoi(getenv("ERGM_ADAMW_NT")) != 0;
+    if (nt)
+        hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
+                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2,
+                           one_m_b2, eps, step_size, bc2_sqrt);
+    else
+        hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
+                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2,
+                           one_m_b2, eps, step_size, bc2_sqrt);
     return check_launch("adamw");
 }
 
