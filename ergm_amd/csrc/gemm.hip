@@ -41,7 +41,7 @@ struct GemmArgs {
     float* slab;        // split-K partials [z][M][N] (f32) or nullptr
     const float* a_scale;  // fp8 GEMM: per-row dequantisation scale of A [M] (nullptr: none)
     const float* b_scale;  // fp8 GEMM: per-column dequantisation scale of B [N]
-    int nt_store;          // bf16 C written with non-temporal stores (streamed output)
+    int nt_store;          // C written with non-temporal stores (streamed output)
 };
 
 template <int EPI, bool OUT_BF16>
@@ -114,8 +114,13 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
             o0.x += p0.x; o0.y += p0.y; o0.z += p0.z; o0.w += p0.w;
             o1.x += p1.x; o1.y += p1.y; o1.z += p1.z; o1.w += p1.w;
         }
-        c[0] = o0;
-        c[1] = o1;
+        if (a.nt_store) {
+            __builtin_nontemporal_store(f32x4{o0.x, o0.y, o0.z, o0.w}, reinterpret_cast<f32x4*>(c));
+            __builtin_nontemporal_store(f32x4{o1.x, o1.y, o1.z, o1.w}, reinterpret_cast<f32x4*>(c + 1));
+        } else {
+            c[0] = o0;
+            c[1] = o1;
+        }
     }
 }
 
@@ -1052,7 +1057,10 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
     // profiles/r01_overlap_experiments.txt #14); ERGM_NT_STORE=0 disables (A/B)
     static const int nt_env = getenv("ERGM_NT_STORE") ? atoi(getenv("ERGM_NT_STORE")) : 1;
-    a.nt_store = nt_env && d->c_dtype == ERGM_BF16 && d->N >= 32768;
+    // ... and so are the f32 weight gradients (A = activationsᵀ), consumed later by the optimizer / the
+    // all-reduce (C5 +0.4-0.8 %, C2 neutral: #17)
+    a.nt_store = nt_env && ((d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
+                            (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE));
     hipStream_t s = as_stream(stream);
     if (p.split > 1) {
         size_t need = (size_t)p.split * d->M * d->N * sizeof(float);
