@@ -61,7 +61,7 @@ def main():
         if gui > 0:
             out["kernels"][name[:110]] = {"dispatches": len(es), "mfma_busy_pct": round(100 * busy / (gui * SIMDS), 2),
                                           "bf16_flops_counted": mops * 512}
-    lm = [k for k in out["kernels"] if "gemm_pipe_kernel<256, 256, 4, 2, 2, false, false, 0, true>" in k]
+    lm = [k for k in out["kernels"] if "gemm_pipe_kernel<256, 256, 4, 2, 2, false, false, 0, true" in k]
     if lm:
         rec = out["kernels"][lm[0]]
         alg = 2.0 * 2048 * 50304 * 768
