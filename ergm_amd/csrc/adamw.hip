@@ -15,6 +15,9 @@ namespace ergm {
 __device__ __forceinline__ void adamw_one(float4& pp, const float4& gg, float4& mm, float4& vv, bf16x4& ob, float decay,
                                           float one_m_b1, float b2, float one_m_b2, float eps, float step_size,
                                           float bc2_sqrt) {
+    // no FMA contraction: every kernel that applies this update (whole buffer, per bucket, per row
+    // selection; temporal or non-temporal memory access) must round identically
+#pragma clang fp contract(off)
     float* P = reinterpret_cast<float*>(&pp);
     const float* G = reinterpret_cast<const float*>(&gg);
     float* Mv = reinterpret_cast<float*>(&mm);
