@@ -69,6 +69,40 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const void* __restrict_
     if (lane == 0) scale[row] = s;
 }
 
+// Rows of at most NCH*512 columns: the row stays in registers (one read), same arithmetic as above.
+template <bool BF16_IN, int NCH>
+__global__ __launch_bounds__(256) void quant_rows_reg_kernel(const void* __restrict__ X, int ldx, int rows, int cols,
+                                                             uint8_t* __restrict__ Q, int ldq, float* __restrict__ scale) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;
+    const size_t base = (size_t)row * ldx;
+    float v[NCH][8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int c = lane * 8 + i * 512;
+        if (c < cols) {
+            load8(X, BF16_IN, base + c, v[i]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[i][j]));
+        }
+    }
+    amax = wave_max(amax);
+    const float s = amax > 0.f ? amax / 448.f : 1.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int c = lane * 8 + i * 512;
+        if (c < cols) {
+            uint2 o;
+            o.x = fp8x4(v[i][0] / s, v[i][1] / s, v[i][2] / s, v[i][3] / s);
+            o.y = fp8x4(v[i][4] / s, v[i][5] / s, v[i][6] / s, v[i][7] / s);
+            *reinterpret_cast<uint2*>(Q + (size_t)row * ldq + c) = o;
+        }
+    }
+    if (lane == 0) scale[row] = s;
+}
+
 // ---- weights: batched over the matrices of one block (WqJobs in common.h) ------------------------
 
 __device__ __forceinline__ int find_job(const WqJobs& J, int bid, bool q) {
@@ -190,8 +224,15 @@ int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void
     ERGM_CHECK_ARG(x_dtype == ERGM_BF16 || x_dtype == ERGM_F32, "quant_rows_fp8: bad dtype");
     dim3 grid(cdiv(rows, 4));
     auto* q = reinterpret_cast<uint8_t*>(Q);
-    if (x_dtype == ERGM_BF16) hipLaunchKernelGGL(quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
-    else hipLaunchKernelGGL(quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+    const int nch = cdiv(cols, 512);
+    if (x_dtype == ERGM_BF16) {
+        if (nch <= 2) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 2>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else if (nch <= 4) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 4>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else if (nch <= 8) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 8>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else hipLaunchKernelGGL(quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+    } else {
+        hipLaunchKernelGGL(quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+    }
     return check_launch("quant_rows_fp8");
 }
 
