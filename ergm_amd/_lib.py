@@ -113,7 +113,9 @@ class ErgmError(RuntimeError):
 
 
 def load(path: str = LIB_PATH):
-    """Load (once) and return the library; raises if it is missing."""
+    """Load (once) and return the library; raises if it is missing.  ERGM_LIB_PATH overrides the path
+    (A/B runs of two builds of the same sources)."""
+    path = os.environ.get("ERGM_LIB_PATH", path)
     global _lib
     with _lock:
         if _lib is None:
