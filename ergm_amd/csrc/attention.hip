@@ -16,9 +16,10 @@
 // atomics, deterministic.  The tiled kernels stream their 64-row tiles through a 3-stage LDS ring filled
 // by LDS-DMA (tiles.h GldsTile: two tiles in flight while one is consumed, one barrier per tile); causal
 // grids start with the longest rows.
-// Sequences of at most 128 (the training path: S = 128 tokens, 128 caption rows) take the
-// *_short kernels instead: one 8-wave workgroup per (b, h) holding every operand in LDS, the whole
-// backward in one launch.  Both paths evaluate every product in the same order (bit-identical).
+// The backward of sequences of at most 128 (the training path: S = 128 tokens, 128 caption rows) takes
+// the fused short kernel instead: one 8-wave workgroup per (b, h) holding every operand in LDS, the whole
+// backward in one launch; it evaluates every product in the same order as the tiled kernels
+// (bit-identical).  The forward is tiled at every length.
 // Softmax arithmetic in the exp2 domain (v_exp_f32 is 2^x): exp(scale·s − shift) = exp2(fma(s, c, −shift·log2e))
 // with c = scale·log2e, one FMA + one v_exp per score; tiles a wave sees entirely unmasked (uniform
 // test per wave and tile) skip the mask compares.
@@ -585,39 +586,6 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
     }
 }
 
-// Forward for Sq, Sk <= 128: one workgroup (8 waves, 16 queries each) per (b, h); K and V staged once.
-template <bool CAUSAL>
-__global__ __launch_bounds__(512) void attn_fwd_short_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) char sK[AS_OPER];
-    __shared__ __attribute__((aligned(16))) char sV[AS_OPER];
-    const int b = blockIdx.z, h = blockIdx.y;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int i16 = lane & 15, g = lane >> 4;
-    const int q = wave * 16 + i16;
-    const __bf16* Qb = a.q + (size_t)b * a.Sq * a.ldq + h * AT_D;
-    bf16x8 qf[2];
-    qf[0] = load_frag_global(Qb, a.ldq, q, a.Sq, 8 * g);
-    qf[1] = load_frag_global(Qb, a.ldq, q, a.Sq, 32 + 8 * g);
-    {
-        const Rows128 rk = load_rows(a.k + (size_t)b * a.Sk * a.ldk + h * AT_D, a.ldk, a.Sk);
-        const Rows128 rv = load_rows(a.v + (size_t)b * a.Sk * a.ldv + h * AT_D, a.ldv, a.Sk);
-        put_rows(sK, rk);
-        put_rows(sV, rv);
-    }
-    __syncthreads();
-    f32x4 o[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, l = 0.f;
-    int nkt = (a.Sk + AT_T - 1) / AT_T;
-    if (CAUSAL) nkt = min(nkt, (wave * 16 + 15) / AT_T + 1);
-    const float c = a.scale * AT_LOG2E;
-    for (int kt = 0; kt < nkt; ++kt)
-        fwd_tile<CAUSAL>(sK + kt * AT_TILE_BYTES, sV + kt * AT_TILE_BYTES, kt * AT_T, q, wave * 16, a.Sk, c, qf, o, m,
-                         l);
-    fwd_store(a, b, h, q, o, m, l);
-}
-
 template <bool CAUSAL>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -810,12 +778,8 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
     a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
     a.scale = 0.125f;  // 1/sqrt(64): exact, so x*scale == x / 8.0 (src/model.py:122-125)
     hipStream_t s = as_stream(stream);
-    if (Sq <= AS_MAX && Sk <= AS_MAX && !g_attn_generic) {
-        dim3 grid(1, H, B);
-        if (causal) hipLaunchKernelGGL(attn_fwd_short_kernel<true>, grid, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL(attn_fwd_short_kernel<false>, grid, dim3(512), 0, s, a);
-        return check_launch("attn_fwd");
-    }
+    // every length takes the tiled kernel: at S = 128 its 2x more workgroups beat the one-workgroup-per-
+    // (b, h) form inside the concurrent step (C2 +1.6 %, C5 +0.4 %; profiles/r01_overlap_experiments.txt #19)
     dim3 grid(cdiv(Sq, AT_T), H, B);
     if (causal) tiled_fwd<true>(grid, s, a);
     else tiled_fwd<false>(grid, s, a);

@@ -135,8 +135,9 @@ int ergm_attn_bwd(const void* q, const void* k, const void* v, const void* o, co
                   const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
                   int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
                   int causal, void* stream);
-/* Path selection hook (tests / tuning): bit 0 of force_generic makes ergm_attn_fwd/bwd use the tiled
- * kernels even where the one-workgroup-per-(b,h) kernels apply (Sq, Sk <= 128); bits 4-7 select the
+/* Path selection hook (tests / tuning): bit 0 of force_generic makes ergm_attn_bwd use the tiled
+ * kernels even where the one-workgroup-per-(b,h) kernel applies (Sq, Sk <= 128; the forward is tiled at
+ * every length); bits 4-7 select the
  * tiled kernels' LDS ring depth (0 = per-kernel defaults; 2, 3 or 4).  Process-wide; not for concurrent use with
  * running attention calls. */
 int ergm_attn_tune(int force_generic);
