@@ -26,6 +26,8 @@
 #include "common.h"
 #include "tiles.h"
 
+#include <cstdlib>
+
 namespace ergm {
 
 constexpr int AT_D = 64;       // head dim
@@ -733,14 +735,16 @@ using namespace ergm;
 
 namespace {
 bool g_attn_generic = false;  // ergm_attn_tune: force the tiled kernels even for short sequences
-int g_attn_ns = 0;            // ergm_attn_tune: ring stages of the tiled kernels (0: per-kernel defaults)
+// ergm_attn_tune: ring stages of the tiled kernels (0: per-kernel defaults); ERGM_ATTN_NS sets the
+// initial value (A/B runs inside the step)
+int g_attn_ns = getenv("ERGM_ATTN_NS") ? atoi(getenv("ERGM_ATTN_NS")) : 0;
 
 template <bool CAUSAL, int NS>
 void launch_tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
     hipLaunchKernelGGL((attn_fwd_kernel<CAUSAL, NS>), grid, dim3(256), 0, s, a);
 }
-// Defaults measured with tools/attn_bench.py at the C4 shape (S = 512): forward and dK/dV 2 stages (the
-// dK/dV kernel then fits 3 waves per SIMD without spills), dQ 3.
+// Defaults: 2 stages everywhere (tools/attn_bench.py at the C4 shape: forward fastest at 2, the dK/dV
+// kernel then fits 3 waves per SIMD without spills; dQ 3 isolated, 2 inside the C4 step, #20).
 template <bool CAUSAL>
 void tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
     if (g_attn_ns == 3) launch_tiled_fwd<CAUSAL, 3>(grid, s, a);
@@ -749,7 +753,7 @@ void tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
 }
 template <bool CAUSAL>
 void tiled_bwd(dim3 gk, dim3 gq, hipStream_t s, const AttnArgs& a) {
-    const int ns_kv = g_attn_ns ? g_attn_ns : 2, ns_q = g_attn_ns ? g_attn_ns : 3;
+    const int ns_kv = g_attn_ns ? g_attn_ns : 2, ns_q = g_attn_ns ? g_attn_ns : 2;
     if (ns_kv == 3) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 3>), gk, dim3(256), 0, s, a);
     else if (ns_kv == 4) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 4>), gk, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 2>), gk, dim3(256), 0, s, a);
