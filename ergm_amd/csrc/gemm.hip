@@ -654,6 +654,7 @@ static constexpr GemmOverride kStepTuned[] = {
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
     {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
     {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+    {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
 };
 
 static bool find_override(const ergm_gemm_desc* d, int& cfg, int& split) {
