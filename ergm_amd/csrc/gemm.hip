@@ -654,6 +654,7 @@ static constexpr GemmOverride kStepTuned[] = {
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
     {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
     {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+    {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
     {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
 };
 
