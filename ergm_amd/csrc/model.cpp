@@ -700,6 +700,23 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
     return ERGM_OK;
 }
 
+// LM-head column split: the vocabulary-wide GEMM runs 256x256 tiles, one per CU per round; the leading
+// n0 columns are the largest multiple of 256 whose tile count fills whole rounds of 256 CUs, the
+// remaining columns (the partial last round) run as a second, small-tile GEMM spread over all CUs.
+// ERGM_LMHEAD_TAIL=0 keeps the single launch.
+int lmhead_split_cols(int T, int Vp) {
+    static const bool on = [] {
+        const char* e = getenv("ERGM_LMHEAD_TAIL");
+        return !(e && e[0] == '0');
+    }();
+    if (!on) return Vp;
+    const int rows = (T + 255) / 256;
+    int q = 256;  // column tiles per whole number of rounds: 256 / gcd(rows, 256)
+    for (int r = rows; r % 2 == 0 && q > 1; r /= 2) q /= 2;
+    const int n0 = (Vp / 256 / q) * q * 256;
+    return (n0 > 0 && Vp - n0 >= 256) ? n0 : Vp;
+}
+
 int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const int T = P->T, E = d.n_embd, L = d.n_layer, B = d.batch, S = d.seq;
@@ -787,8 +804,13 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
     {
         Probe pr(P, 1, s);
-        ERGM_TRY(gemm(P, s, T, d.vocab_pad, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
+        const int n0 = lmhead_split_cols(T, d.vocab_pad);
+        ERGM_TRY(gemm(P, s, T, n0, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
                       ERGM_BF16, ERGM_EPI_NONE));
+        if (n0 < d.vocab_pad)
+            ERGM_TRY(gemm(P, s, T, d.vocab_pad - n0, E, P->lnf, E, ERGM_MK,
+                          reinterpret_cast<const __bf16*>(p.wte_b) + (size_t)n0 * E, E, ERGM_NK,
+                          reinterpret_cast<__bf16*>(logits) + n0, d.vocab_pad, ERGM_BF16, ERGM_EPI_NONE));
     }
     if (P->dry) return ERGM_OK;
     ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, P->emo_tmp,
