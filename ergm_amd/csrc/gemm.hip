@@ -725,9 +725,10 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
         const bool km = d->a_layout == ERGM_KM;
         if (K >= 32768 && t128 < 240 && d->split_k != 1) {
             // contraction over the vocabulary (LM-head dX) / the stacked caption K/V at config 5: the
-            // 256x256 tile, split until ~256 workgroups (tools/gemm_tune.py: c6s8 at C2, c6s4 at C5)
+            // 256x256 tile, split until ~256 workgroups (c6s10 at C2: 240 workgroups, LM-head dX 195 -> 172
+            // us in-step, profiles/r01_lmhead_probe.txt; c6s5 at C4, c6s4 at C5)
             p.cfg = 6;
-            split = (int)std::max(1L, std::min(8L, 256 / std::max(1L, tiles_of(M, N, 256, 256))));
+            split = (int)std::max(1L, std::min(16L, 256 / std::max(1L, tiles_of(M, N, 256, 256))));
         } else if (K >= 4096 && t128 < 240 && d->split_k != 1) {
             p.cfg = 2;
             // weight gradients over T >= 4096 tokens (config 5): split only the smallest outputs
