@@ -29,6 +29,19 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
+def lmhead_split_cols(T: int, Vp: int) -> int:
+    """Columns of the LM head's main launch (model.cpp lmhead_split_cols): the largest multiple of 256
+    whose 256x256 tiles fill whole rounds of 256 CUs; the rest runs as a small-tile tail launch."""
+    if os.environ.get("ERGM_LMHEAD_TAIL", "1")[:1] == "0":
+        return Vp
+    rows, q = -(-T // 256), 256
+    while rows % 2 == 0 and q > 1:
+        rows //= 2
+        q //= 2
+    n0 = (Vp // 256 // q) * q * 256
+    return n0 if n0 > 0 and Vp - n0 >= 256 else Vp
+
+
 def pmc_traffic(probe: int, config: str = "c2"):
     """HBM bytes per launch of the probed kernel from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from separate rocprofv3
@@ -222,9 +235,14 @@ def main():
     ms_step = 1000.0 * dt / args.steps
     T = B * S
     V, E = cfg.vocab_size, cfg.n_embd
-    probe_flops = {1: 2.0 * T * V * E, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
+    Vp = model.layout.vocab_pad
+    n0 = min(V, lmhead_split_cols(T, Vp))
+    probe_flops = {1: 2.0 * T * n0 * E, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
                    4: 2.0 * T * E * (2 * E * cfg.n_layer)}[args.probe]
-    probe_name = {1: "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
+    probe_name = {1: f"LM-head forward main GEMM [T,E]x[E,{n0}] (pipelined MFMA GEMM, 256x256 tiles in whole "
+                     f"rounds of 256 CUs, bf16 out; the last {Vp - n0} vocabulary columns run as a "
+                     "separate small-tile launch)" if n0 < V else
+                  "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
                   2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
     achieved = probe_flops / (probe_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(args.probe, args.config)

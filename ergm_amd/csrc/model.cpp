@@ -803,10 +803,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
     {
-        Probe pr(P, 1, s);
         const int n0 = lmhead_split_cols(T, d.vocab_pad);
-        ERGM_TRY(gemm(P, s, T, n0, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
-                      ERGM_BF16, ERGM_EPI_NONE));
+        {
+            Probe pr(P, 1, s);  // the bench's roofline kernel: the whole-round main launch
+            ERGM_TRY(gemm(P, s, T, n0, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
+                          ERGM_BF16, ERGM_EPI_NONE));
+        }
         if (n0 < d.vocab_pad)
             ERGM_TRY(gemm(P, s, T, d.vocab_pad - n0, E, P->lnf, E, ERGM_MK,
                           reinterpret_cast<const __bf16*>(p.wte_b) + (size_t)n0 * E, E, ERGM_NK,

@@ -64,7 +64,9 @@ def main():
     lm = [k for k in out["kernels"] if "gemm_pipe_kernel<256, 256, 4, 2, 2, false, false, 0, true" in k]
     if lm:
         rec = out["kernels"][lm[0]]
-        alg = 2.0 * 2048 * 50304 * 768
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import lmhead_split_cols
+        alg = 2.0 * 2048 * lmhead_split_cols(2048, 50304) * 768  # the main launch (bench's roofline kernel)
         out["lm_head_fwd"] = dict(rec, algorithmic_flops=alg, counted_over_algorithmic=rec["bf16_flops_counted"] / alg)
     top = sorted(out["kernels"].items(), key=lambda kv: -kv[1]["mfma_busy_pct"])[:12]
     for k, v in top:

@@ -61,10 +61,12 @@ def main():
 
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of bench.py; "
                      "FETCH_SIZE doubled (gfx950 streaming-read correction), KiB -> bytes; median over dispatches"}
-    lm = pick(lambda k: "gemm_pipe_kernel<256, 256" in k)
+    lm = pick(lambda k: "gemm_pipe_kernel<256, 256, 4, 2, 2, false, false, 0, true" in k)
     if lm:
         k, fb, wb = lm
-        alg = 2 * T * E + 2 * Vp * E + 2 * T * Vp   # A [T,E] + wte [Vp,E] bf16 read, logits [T,Vp] bf16 written
+        from bench import lmhead_split_cols
+        n0 = lmhead_split_cols(T, Vp)  # the main launch's columns (the bench's roofline kernel)
+        alg = 2 * T * E + 2 * n0 * E + 2 * T * n0   # A [T,E] + wte [n0,E] bf16 read, logits [T,n0] bf16 written
         res["lm_head_fwd"] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                               "algorithmic_bytes": alg, "ratio": (fb + wb) / alg}
     ad = pick(lambda k: "adamw_kernel" in k)
