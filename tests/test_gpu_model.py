@@ -233,3 +233,31 @@ def test_iemocap_shape_long_sequence_matches_oracle(gpu):
     ref_loss = float(ref["loss"])
     assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
     _grad_gate(_grads(model), og)
+
+
+def test_full_vocab_lm_head_at_c2_token_count(gpu):
+    """The LM head at C2's token count (T = 16·128 = 2048) over the real 50260-word vocabulary: the
+    forward runs as the whole-round main launch (49152 columns) + the 1152-column tail launch, and the
+    vocabulary-deep dX as a 10-way split (profiles/r01_lmhead_probe.txt).  One block keeps the oracle
+    quick; every logit (main and tail columns), the loss and every gradient against the oracle."""
+    import bench
+    from ergm_amd.data import synthetic_batch
+    V, E, Lyr, H = 50260, 768, 1, 12
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    P0 = O.init_params(ocfg, seed=11)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    Vp = model.layout.vocab_pad
+    n0 = bench.lmhead_split_cols(2048, Vp)
+    assert n0 < V < Vp, (n0, V, Vp)  # the split path is the one under test
+    batch = synthetic_batch(16, 128, n_turns=5, feat_dim=E, seed=12)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    lg = out.logits.float().cpu()
+    rl = ref["logits"]
+    assert (lg[..., :n0] - rl[..., :n0]).abs().max().item() <= LOGIT_ATOL
+    assert (lg[..., n0:V] - rl[..., n0:V]).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), og)
