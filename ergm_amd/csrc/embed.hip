@@ -54,45 +54,78 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
     }
 }
 
-constexpr int SORT_MAX = 16384;  // entries handled by the single-workgroup LDS sort (128 KiB of u64)
+constexpr int SORT_MAX = 16384;  // entries one workgroup sorts in LDS (128 KiB of u64)
 
-// keys = (vocab id << 32) | entry, entry in [0, 3T): [0,T) input ids, [T,2T) token types, [2T,3T) captions
-// row_flag (optional, pre-zeroed, one byte per vocab row): set to 1 for every row the lookups touch.
+// keys = (vocab id << 32) | entry, entry in [0, 3T): [0,T) input ids, [T,2T) token types, [2T,3T) captions,
+// sorted ascending over npad = next_pow2(3T) slots (padding keys ~0 sort last) by a bitonic network.
+// One workgroup per chunk of `chunk` = min(npad, SORT_MAX) slots runs every compare of the network that
+// stays inside its chunk, in LDS: merge_size = 0 generates the chunk's keys from the ids and runs stages
+// 2..chunk; merge_size > chunk loads the chunk and runs the strides < chunk of that stage (the larger
+// strides are embed_sort_global_kernel passes).  Directions come from global indices, so the chunks
+// compose into the one global network (and a single chunk is the whole sort).  Slots g < n_out are
+// written back; row_flag (optional, pre-zeroed, one byte per vocab row), on the last launch only, is set
+// for every row the lookups touch.
 __global__ __launch_bounds__(1024) void embed_sort_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
-                                                          const int64_t* __restrict__ cap_ids, int T, int V, int npad,
-                                                          uint64_t* __restrict__ out, uint8_t* __restrict__ row_flag) {
+                                                          const int64_t* __restrict__ cap_ids, int T, int V, int chunk,
+                                                          int merge_size, uint64_t* __restrict__ out, int n_out,
+                                                          uint8_t* __restrict__ row_flag) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint64_t* key = reinterpret_cast<uint64_t*>(smem);
     const int n = 3 * T;
-    for (int i = threadIdx.x; i < npad; i += 1024) {
+    const int base = blockIdx.x * chunk;
+    for (int i = threadIdx.x; i < chunk; i += 1024) {
+        const int g = base + i;
         uint64_t k = ~0ull;
-        if (i < n) {
-            int src = i / T, t = i - src * T;
+        if (merge_size) {
+            k = out[g];
+        } else if (g < n) {
+            int src = g / T, t = g - src * T;
             int64_t id = src == 0 ? ids[t] : (src == 1 ? (tt ? tt[t] : -1) : cap_ids[t]);
-            if (id >= 0 && id < V) k = ((uint64_t)id << 32) | (uint64_t)i;
+            if (id >= 0 && id < V) k = ((uint64_t)id << 32) | (uint64_t)g;
         }
         key[i] = k;
     }
     __syncthreads();
-    for (int size = 2; size <= npad; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < npad / 2; i += 1024) {
-                int lo = 2 * i - (i & (stride - 1));
-                int hi = lo + stride;
-                bool up = (lo & size) == 0;
-                uint64_t a = key[lo], b = key[hi];
-                if ((a > b) == up) {
-                    key[lo] = b;
-                    key[hi] = a;
-                }
+    auto stage = [&](int size, int stride) {
+        for (int i = threadIdx.x; i < chunk / 2; i += 1024) {
+            int lo = 2 * i - (i & (stride - 1));
+            int hi = lo + stride;
+            bool up = ((base + lo) & size) == 0;
+            uint64_t a = key[lo], b = key[hi];
+            if ((a > b) == up) {
+                key[lo] = b;
+                key[hi] = a;
             }
-            __syncthreads();
         }
+        __syncthreads();
+    };
+    if (merge_size) {
+        for (int stride = chunk >> 1; stride > 0; stride >>= 1) stage(merge_size, stride);
+    } else {
+        for (int size = 2; size <= chunk; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) stage(size, stride);
     }
-    for (int i = threadIdx.x; i < n; i += 1024) {
+    for (int i = threadIdx.x; i < chunk; i += 1024) {
+        const int g = base + i;
+        if (g >= n_out) continue;
         const uint64_t k = key[i];
-        out[i] = k;
+        out[g] = k;
         if (row_flag && k != ~0ull) row_flag[k >> 32] = 1;
+    }
+}
+
+// one compare-exchange step of stage `size` at a stride >= the chunk (pairs span chunks)
+__global__ __launch_bounds__(256) void embed_sort_global_kernel(uint64_t* __restrict__ key, int npad, int size,
+                                                                int stride) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= npad / 2) return;
+    const int lo = 2 * i - (i & (stride - 1));
+    const int hi = lo + stride;
+    const bool up = (lo & size) == 0;
+    const uint64_t a = key[lo], b = key[hi];
+    if ((a > b) == up) {
+        key[lo] = b;
+        key[hi] = a;
     }
 }
 
@@ -293,7 +326,12 @@ extern "C" int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64
     return embed_fwd_ld(ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cap, E, B, S, E, V, as_stream(stream));
 }
 
-static size_t keys_bytes(int T) { return ((size_t)3 * T * sizeof(uint64_t) + 255) & ~(size_t)255; }
+namespace ergm {
+// sorted-key slots: 3T when one workgroup sorts them all, else the padded network width
+int embed_sort_capacity(int T) { return 3 * T <= SORT_MAX ? 3 * T : next_pow2(3 * T); }
+}  // namespace ergm
+
+static size_t keys_bytes(int T) { return ((size_t)embed_sort_capacity(T) * sizeof(uint64_t) + 255) & ~(size_t)255; }
 
 extern "C" size_t ergm_embed_bwd_workspace_size(int T) {
     // sorted keys + one partial row per sorted position (run sums); E <= 1024
@@ -306,7 +344,7 @@ namespace ergm {
 int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
                    uint8_t* row_flag, int n_flag, hipStream_t s) {
     ERGM_CHECK_ARG(ids && cap_ids && keys, "embed_bwd: null argument");
-    ERGM_CHECK_ARG(3 * T <= SORT_MAX, "embed_bwd: 3*B*S=%d exceeds the single-workgroup sort (%d)", 3 * T, SORT_MAX);
+    ERGM_CHECK_ARG(T > 0 && 3 * T <= (1 << 30), "embed_bwd: bad token count %d", T);
     ERGM_CHECK_ARG(!row_flag || n_flag >= V, "embed_bwd: row_flag shorter than the vocabulary");
     static bool attr_set = false;  // benign race: idempotent attribute write
     if (!attr_set) {
@@ -317,9 +355,20 @@ int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
     }
     if (row_flag && hipMemsetAsync(row_flag, 0, (size_t)n_flag, s) != hipSuccess)
         return fail(ERGM_EHIP, "embed_bwd: memset");
-    const int npad = next_pow2(3 * T);
-    hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), (size_t)npad * sizeof(uint64_t), s, ids, tt, cap_ids, T,
-                       V, npad, keys, row_flag);
+    const int n = 3 * T, npad = next_pow2(n);
+    const int chunk = std::min(npad, SORT_MAX), nch = npad / chunk;
+    const size_t lds = (size_t)chunk * sizeof(uint64_t);
+    // (keys holds embed_sort_capacity(T) slots: n for one chunk, npad for several)
+    hipLaunchKernelGGL(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, 0, keys,
+                       nch > 1 ? npad : n, nch > 1 ? nullptr : row_flag);
+    for (int size = 2 * chunk; size <= npad; size <<= 1) {
+        for (int stride = size >> 1; stride >= chunk; stride >>= 1)
+            hipLaunchKernelGGL(embed_sort_global_kernel, dim3(cdiv(npad / 2, 256)), dim3(256), 0, s, keys, npad, size,
+                               stride);
+        const bool last = size == npad;
+        hipLaunchKernelGGL(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, size, keys,
+                           last ? n : npad, last ? row_flag : nullptr);
+    }
     return check_launch("embed_bwd_sort");
 }
 

@@ -42,6 +42,7 @@ int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, 
                  int V, hipStream_t s);
 int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
                    uint8_t* row_flag, int n_flag, hipStream_t s);
+int embed_sort_capacity(int T);
 int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
                    float* dwpe, float* part, const int* row_pos, hipStream_t s);
 int feat_pack(const float* vis, int ld_vis, const float* aud, void* out, int B, int Bp, int Fd, int ld, hipStream_t s);
@@ -235,7 +236,7 @@ size_t carve(ergm_model_plan* P, char* base) {
         P->proj_out = nullptr;
         P->dproj = nullptr;
     }
-    P->keys = c.take<uint64_t>(3 * T);
+    P->keys = c.take<uint64_t>(embed_sort_capacity(T));
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
     P->d_o = c.take<__bf16>(T * E);

@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restr
     __syncthreads();
     if (threadIdx.x == 0) {
         float lm = ((red[0] + red[1]) + red[2]) + red[3];
-        lm = n_valid ? lm / (float)max(1, *n_valid) : 0.f;
+        // mean over the valid labels; none valid gives 0/0 = NaN, as torch's CrossEntropyLoss does for the
+        // reference (src/model.py:704-709; the dlogits of ignored rows stay 0, as its gradient does)
+        lm = n_valid ? lm / (float)(*n_valid) : 0.f;
         float emo = emo_sum ? *emo_sum / (float)B_global : 0.f;
         out[0] = lm;
         out[1] = emo;

@@ -261,3 +261,49 @@ def test_full_vocab_lm_head_at_c2_token_count(gpu):
     assert (lg[..., :n0] - rl[..., :n0]).abs().max().item() <= LOGIT_ATOL
     assert (lg[..., n0:V] - rl[..., n0:V]).abs().max().item() <= LOGIT_ATOL
     _grad_gate(_grads(model), og)
+
+
+def _small_model(gpu, S, seed, V=512, E=128, Lyr=2, H=2):
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    P0 = O.init_params(ocfg, seed=seed)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    return ocfg, P0, model
+
+
+@pytest.mark.parametrize("B,S", [(1, 1024), (8, 1023)])
+def test_maximum_length_matches_oracle(gpu, B, S):
+    """The longest sequence the reference can take (n_positions = 1024, every wpe row used; 1023 = the
+    longest sample CustomDataset keeps, src/custom_dataset.py:51, with ragged attention tiles; the
+    executor needs B*S % 8 == 0, hence B = 8 there): loss, every logit and every gradient against the
+    oracle."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    ocfg, P0, model = _small_model(gpu, S, seed=21)
+    batch = synthetic_batch(B, S, n_turns=20, feat_dim=E, seed=22, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), og)
+
+
+def test_all_labels_ignored_matches_reference(gpu):
+    """No valid LM label in the batch (every label -100): the reference's mean cross-entropy is 0/0 =
+    NaN (torch CrossEntropyLoss, src/model.py:704-709), so is its total loss; the LM part contributes
+    no gradient and the emotion head's gradient is unchanged.  The fused step matches all three."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    ocfg, P0, model = _small_model(gpu, 64, seed=23)
+    batch = synthetic_batch(2, 64, n_turns=3, feat_dim=E, seed=24, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+    batch["labels"] = torch.full_like(batch["labels"], -100)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    assert torch.isnan(ref["loss"]).item()
+    assert torch.isnan(out.loss).item()
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    assert (out.emotion_logits.float().cpu() - ref["emotion_logits"]).abs().max().item() <= LOGIT_ATOL
+    assert torch.isfinite(model.flat.grad).all().item()
+    _grad_gate(_grads(model), og)
