@@ -273,7 +273,11 @@ typedef enum {
     ERGM_T_LN2_W, ERGM_T_LN2_B, ERGM_T_FC_W, ERGM_T_FC_B, ERGM_T_MPROJ_W, ERGM_T_MPROJ_B,
 } ergm_layer_tensor;
 
-/* Bytes of device workspace the executor needs (activations saved for backward + scratch). */
+/* Bytes of device workspace the executor needs (activations saved for backward + scratch).
+ * Shape rules: batch * seq % 8 == 0 (the weight-gradient GEMMs contract over the B*S tokens in steps
+ * of 8; every config of the reference's launchers - batch 16 / 8 - satisfies it, and PadCollate's
+ * pad_multiple option pads a batch's length so that any batch does), 2 <= seq <= n_positions,
+ * n_head * 64 == n_embd <= 1024, n_inner and feat_dim multiples of 64; ERGM_EINVAL otherwise. */
 size_t ergm_model_workspace_size(const ergm_model_dims* dims);
 int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* workspace,
                       size_t ws_bytes, ergm_model_plan** out_plan);
