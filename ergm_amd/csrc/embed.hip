@@ -373,10 +373,9 @@ int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
 }
 
 // dwte[id] += Σ (ordered) of the lookup gradients of each sorted run; dwpe = Σ_b dh0[b].
-// part: 3T x E floats of scratch.
+// part: 3T x E floats of scratch (reused, once the runs are summed, by the dwpe column sums).
 int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, const float* dcap, float* dwte,
                    float* dwpe, float* part, const int* row_pos, hipStream_t s) {
-    ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
     const int T = B * S, n = 3 * T;
     dim3 g1(cdiv(n, SEG_CH)), g2(n);
 #define ERGM_SEG(NC)                                                                                         \
@@ -391,7 +390,7 @@ int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, 
 #undef ERGM_SEG
     ERGM_TRY(check_launch("embed_bwd"));
     // dwpe[s][e] = Σ_b dh0[b][s][e]   (rows b of [B][S*E])
-    return colsum_impl(dh0, false, B, S * E, S * E, dwpe, 0, nullptr, 0, s);
+    return colsum_impl(dh0, false, B, S * E, S * E, dwpe, 0, part, (size_t)n * E * sizeof(float), s);
 }
 }  // namespace ergm
 
@@ -402,7 +401,6 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
     ERGM_CHECK_ARG(B > 0 && S > 0 && E > 0 && E % 4 == 0 && E <= 1024, "embed_bwd: bad shape");
     const int T = B * S;
     ERGM_CHECK_ARG(ws && ws_bytes >= ergm_embed_bwd_workspace_size(T), "embed_bwd: workspace too small");
-    ERGM_CHECK_ARG(B <= 64, "embed_bwd: batch > 64 needs a colsum workspace");
     hipStream_t s = as_stream(stream);
     uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
     ERGM_TRY(embed_bwd_sort(ids, tt, cap_ids, T, V, keys, nullptr, 0, s));

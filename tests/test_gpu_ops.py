@@ -277,10 +277,10 @@ def test_colsum(gpu, rows, cols, dt):
     assert _rel(out2, 2 * X.double().sum(0)) < 1e-6
 
 
-@pytest.mark.parametrize("B,S", [(8, 1023), (16, 1024), (32, 512)])
+@pytest.mark.parametrize("B,S", [(8, 1023), (16, 1024), (32, 512), (128, 64), (96, 40)])
 def test_embedding_bwd_multi_workgroup_sort(gpu, B, S):
     """3·B·S above the one-workgroup LDS sort (16384 entries): the lookups are sorted by chunked
-    LDS stages + global compare-exchange passes.  Gradients against fp64 index_add (the sums of the
+    LDS stages + global compare-exchange passes; batches above 64 (multi-block wpe column sums).  Gradients against fp64 index_add (the sums of the
     ~B·S/2 token-type collisions per row included) and bitwise run to run."""
     E, V = 128, 50304
     g = torch.Generator().manual_seed(B * S)
