@@ -1020,7 +1020,10 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
                          size_t ws_bytes, void* stream) {
     ERGM_CHECK_ARG(d && A && B && C, "ergm_gemm: null argument");
     ERGM_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "ergm_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
-    ERGM_CHECK_ARG(d->K % 8 == 0, "ergm_gemm: K=%d must be a multiple of 8", d->K);
+    // k-contiguous operands are read in 8-element chunks along K; with both operands k-major (rows = k,
+    // the weight-gradient layout) any K works
+    ERGM_CHECK_ARG(d->K % 8 == 0 || (d->a_layout == ERGM_KM && d->b_layout == ERGM_KN),
+                   "ergm_gemm: K=%d must be a multiple of 8 unless a_layout = KM and b_layout = KN", d->K);
     ERGM_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "ergm_gemm: lda/ldb must be multiples of 8 elements");
     ERGM_CHECK_ARG(aligned16(A) && aligned16(B), "ergm_gemm: A/B must be 16-byte aligned");
     ERGM_CHECK_ARG(d->a_layout == ERGM_MK || d->a_layout == ERGM_KM, "ergm_gemm: bad a_layout");

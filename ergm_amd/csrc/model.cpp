@@ -445,7 +445,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     ERGM_CHECK_ARG(d.n_inner % 64 == 0, "model_create: n_inner must be a multiple of 64");
     ERGM_CHECK_ARG(d.vocab > 0 && d.vocab_pad >= d.vocab && d.vocab_pad % 64 == 0, "model_create: bad vocab_pad");
     ERGM_CHECK_ARG(d.batch > 0 && d.seq >= 2 && d.seq <= d.n_positions, "model_create: bad batch/seq");
-    ERGM_CHECK_ARG((d.batch * d.seq) % 8 == 0, "model_create: B*S must be a multiple of 8");
     ERGM_CHECK_ARG(d.n_layer > 0, "model_create: n_layer must be > 0");
     ERGM_CHECK_ARG(d.feat_dim >= 0 && d.feat_dim % 64 == 0, "model_create: feat_dim must be a multiple of 64");
     ERGM_CHECK_ARG(!d.fp8 || (d.n_embd % 128 == 0 && d.n_inner % 128 == 0 && params->capkv_w),

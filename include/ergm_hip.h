@@ -274,10 +274,9 @@ typedef enum {
 } ergm_layer_tensor;
 
 /* Bytes of device workspace the executor needs (activations saved for backward + scratch).
- * Shape rules: batch * seq % 8 == 0 (the weight-gradient GEMMs contract over the B*S tokens in steps
- * of 8; every config of the reference's launchers - batch 16 / 8 - satisfies it, and PadCollate's
- * pad_multiple option pads a batch's length so that any batch does), 2 <= seq <= n_positions,
- * n_head * 64 == n_embd <= 1024, n_inner and feat_dim multiples of 64; ERGM_EINVAL otherwise. */
+ * Shape rules: 2 <= seq <= n_positions, any batch (token counts B*S that are not multiples of 64 run
+ * the weight-gradient GEMMs on the register-staged kernel), n_head * 64 == n_embd <= 1024, n_inner and
+ * feat_dim multiples of 64; ERGM_EINVAL otherwise. */
 size_t ergm_model_workspace_size(const ergm_model_dims* dims);
 int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* params, void* workspace,
                       size_t ws_bytes, ergm_model_plan** out_plan);

@@ -307,3 +307,22 @@ def test_all_labels_ignored_matches_reference(gpu):
     assert (out.emotion_logits.float().cpu() - ref["emotion_logits"]).abs().max().item() <= LOGIT_ATOL
     assert torch.isfinite(model.flat.grad).all().item()
     _grad_gate(_grads(model), og)
+
+
+@pytest.mark.parametrize("B,S,feat", [(3, 37, True), (1, 2, False), (5, 61, True)])
+def test_odd_token_counts_match_oracle(gpu, B, S, feat):
+    """Batches whose token count B*S is odd / not a multiple of 8 or 64 (PadCollate pads a batch to
+    its longest utterance, src/custom_dataset.py:120-122, so any length occurs): the weight-gradient
+    GEMMs contract over B*S tokens on the register-staged kernel.  Loss, logits and every gradient
+    against the oracle."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    ocfg, P0, model = _small_model(gpu, S, seed=31 + S)
+    batch = synthetic_batch(B, S, n_turns=2 if S < 8 else 3, feat_dim=E, seed=32 + S, vocab_hi=V - 3, sp1=V - 2,
+                            sp2=V - 1, eos=V - 4, with_features=feat)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), og)
