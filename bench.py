@@ -116,6 +116,43 @@ def cpu_baseline(S, turns, B, model="small", feat_dim=768, seconds_target=20.0):
                       f"GPT-2-{model}+fusion, after 1 warm-up step; torch CPU threads={n}"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` without an external launcher: start N fresh rank processes of this script (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment)
+    and return the first non-zero exit status.  The parent never touches the GPU (no HIP call before
+    the children exist); rank 0's stdout carries the JSON line.  A failing rank ends the others."""
+    import subprocess
+    env0 = dict(os.environ)
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    port = env0.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, ERGM_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # exact PIDs this launcher started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,29 +166,49 @@ def main():
                     help="grid cap of the overlapped per-bucket AdamW (default: FusedAdamW.overlap_blocks)")
     ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch: one fresh process per GPU, before anything here initialises HIP
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
-    # rehearsal hook (one-GPU box): ERGM_BENCH_REHEARSE=1 puts every rank on cuda:0 and uses gloo, so the
-    # data-parallel path of this script runs end to end without a GPU per rank (numbers not meaningful)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
+    if os.environ.get("ERGM_BENCH_LAUNCH_PROBE") == "1":
+        # CPU test hook (tests/test_bench_launch.py): the ranks rendezvous over gloo and report, no GPU
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"world_size": dist.get_world_size(), "rank_sum": t.item(),
+                              "local_ranks": os.environ.get("LOCAL_RANK")}), flush=True)
+        dist.destroy_process_group()
+        return
+    # rehearsal hook (one-GPU box): ERGM_BENCH_REHEARSE=1 puts every rank on cuda:0 and uses gloo (RCCL
+    # refuses two ranks on one device), so the data-parallel path of this script runs end to end
+    # without a GPU per rank (numbers not meaningful)
     rehearse = os.environ.get("ERGM_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
+        backend = args.backend or ("gloo" if rehearse else "nccl")
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
+        got = dist.get_world_size()
+        if got != args.gpus:
+            raise SystemExit(f"rank {rank}: process group has {got} ranks, --gpus {args.gpus}")
 
     from ergm_amd import _lib
     from ergm_amd.config import ERGMConfig
@@ -276,6 +333,8 @@ def main():
                                                          0)},
         "optimizer": "FusedAdamW " + (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks})"
                                       if not args.no_overlap_optim else "after backward"),
+        "world_size": world,
+        "dp": {"backend": backend, "rehearsal": rehearse} if world > 1 else None,
         "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
         "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
                           "emotion_acc": round(correct.item() / (B * total), 4)},

@@ -13,6 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
+ABI_VERSION = 3  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -25,12 +26,18 @@ LAYER_TENSORS = ["ln_1.weight", "ln_1.bias", "attn.c_attn.weight", "attn.c_attn.
                  "mlp.c_proj.weight", "mlp.c_proj.bias"]  # order of ergm_layer_tensor
 
 
+class Dropout(C.Structure):
+    """ergm_dropout: one dropout site of one forward (ergm_hip.h)."""
+    _fields_ = [("seed", C.c_uint64), ("offset", C.c_uint32), ("site", C.c_uint32), ("p", C.c_float),
+                ("row0", C.c_int64)]
+
+
 class GemmDesc(C.Structure):
     _fields_ = [("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
                 ("ldc", C.c_int), ("a_layout", C.c_int), ("b_layout", C.c_int), ("c_dtype", C.c_int),
                 ("epilogue", C.c_int), ("alpha", C.c_float), ("bias", C.c_void_p), ("aux", C.c_void_p),
                 ("ld_aux", C.c_int), ("aux_out", C.c_void_p), ("ld_aux_out", C.c_int), ("split_k", C.c_int),
-                ("alpha_dev", C.c_void_p)]
+                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout))]
 
 
 class ModelDims(C.Structure):
@@ -66,22 +73,24 @@ _SIGS = {
     "ergm_gemm_f8_tune": (i32, [i32]),
     "ergm_quant_rows_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp]),
     "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp]),
-    "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "ergm_attn_tune": (i32, [i32]),
-    "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp]),
+    "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp, vp, vp]),
     "ergm_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, f32, vp]),
     "ergm_layernorm_bwd_workspace_size": (sz, [i32, i32]),
-    "ergm_layernorm_bwd": (i32, [vp] * 10 + [sz, i32, i32, vp]),
+    "ergm_layernorm_bwd": (i32, [vp] * 10 + [sz, i32, i32, vp, vp]),
+    "ergm_dropout_mask": (i32, [vp, i32, i32, vp, vp]),
+    "ergm_dropout_apply": (i32, [vp, vp, i32, i32, i32, vp]),
     "ergm_colsum_workspace_size": (sz, [i32, i32]),
     "ergm_colsum": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
-    "ergm_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "ergm_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     "ergm_feat_pool": (i32, [vp, i32, i32, i32, i32, C.c_long, C.c_long, vp, vp, i32, vp]),
     "ergm_embed_bwd_workspace_size": (sz, [i32]),
     "ergm_embed_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, vp]),
-    "ergm_count_valid": (i32, [vp, i32, i32, vp, vp]),
+    "ergm_count_valid": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
     "ergm_xent_fwd_bwd": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
-    "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
-    "ergm_loss_finalize": (i32, [vp, i32, vp, vp, i32, vp, vp]),
+    "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    "ergm_loss_finalize": (i32, [vp, i32, vp, vp, vp, vp, vp]),
     "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
     "ergm_adamw_rows": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, i32, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
@@ -94,7 +103,8 @@ _SIGS = {
     "ergm_model_set_lookup_compact": (i32, [vp, vp, vp]),
     "ergm_rows_scan": (i32, [vp, i32, vp, vp, vp]),
     "ergm_rows_compact": (i32, [vp, vp, i32, i32, vp, vp, i32, vp]),
-    "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
+    "ergm_model_set_inputs": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "ergm_model_set_dropout": (i32, [vp, f32, f32, f32, C.c_uint64, C.c_uint32, i32]),
     "ergm_model_forward": (i32, [vp, vp, vp, vp, i32, vp]),
     "ergm_model_backward_head": (i32, [vp, vp, vp]),
     "ergm_model_backward_layer": (i32, [vp, i32, vp]),
@@ -127,6 +137,9 @@ def load(path: str = LIB_PATH):
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            if lib.ergm_version() != ABI_VERSION:
+                raise ErgmError(f"{path} has ABI {lib.ergm_version()}, this binding expects {ABI_VERSION}: rebuild "
+                                "with `python -m ergm_amd.build`")
             _lib = lib
     return _lib
 

@@ -19,7 +19,7 @@ BUILD = os.path.join(REPO, "build")
 LIB = os.path.join(HERE, "libergm_hip.so")
 ARCH = os.environ.get("ERGM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm.hip", "embed.hip", "xent.hip", "adamw.hip", "quant.hip", "model.cpp"]
+SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm.hip", "embed.hip", "xent.hip", "adamw.hip", "quant.hip", "dropout.hip", "model.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable"]
 

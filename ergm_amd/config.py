@@ -30,10 +30,11 @@ class ERGMConfig:
     n_inner: Optional[int] = None
     layer_norm_epsilon: float = 1e-5
     initializer_range: float = 0.02
-    # dropout probabilities: the build runs the deterministic (p=0) path, as the parity oracle does
-    attn_pdrop: float = 0.0
-    resid_pdrop: float = 0.0
-    embd_pdrop: float = 0.0
+    # dropout probabilities (GPT2Config defaults = the "gpt2" checkpoint the reference fine-tunes,
+    # src/main.py:62): applied in train() mode; 0 gives the deterministic path the parity goldens use
+    attn_pdrop: float = 0.1
+    resid_pdrop: float = 0.1
+    embd_pdrop: float = 0.1
     # width of the pooled audio / visual features (data_process/feature_extraction.py:63,69 → 768).
     # When it differs from n_embd a build-side projection GEMM maps it (config 5).
     feat_dim: Optional[int] = None
@@ -54,8 +55,10 @@ class ERGMConfig:
             # same message family as src/model.py:81-85
             raise ValueError(f"`embed_dim` must be divisible by num_heads (got `embed_dim`: {self.n_embd} "
                              f"and `num_heads`: {self.n_head}).")
-        if self.attn_pdrop or self.resid_pdrop or self.embd_pdrop:
-            raise ValueError("dropout > 0 is not supported by the fused HIP path (deterministic parity path)")
+        for name in ("attn_pdrop", "resid_pdrop", "embd_pdrop"):
+            p = getattr(self, name)
+            if not 0.0 <= p < 1.0:
+                raise ValueError(f"{name} must be in [0, 1) (got {p})")
 
     def to_dict(self):
         return asdict(self)
@@ -67,3 +70,7 @@ def gpt2_small(**kw) -> ERGMConfig:
 
 def gpt2_medium(**kw) -> ERGMConfig:
     return ERGMConfig(n_embd=1024, n_layer=24, n_head=16, **kw)
+
+
+# the deterministic path (every dropout off): parity goldens / oracle comparisons without mask replay
+NO_DROPOUT = dict(attn_pdrop=0.0, resid_pdrop=0.0, embd_pdrop=0.0)

@@ -33,6 +33,7 @@ namespace ergm {
 constexpr int AT_D = 64;       // head dim
 constexpr int AT_T = 64;       // tile rows (queries or keys)
 constexpr int AT_TILE_BYTES = AT_T * AT_D * 2;  // 8 KiB
+constexpr int AT_MAX_SQ_DROP = 1024;            // dropout: keep-bit words a tiled backward stages in LDS
 
 // 64x64 bf16 tile in LDS, 128-B rows, 16-B chunk c of row r stored at chunk c ^ (r & 7):
 // conflict-free for both ds_read_b128 row reads and the ds_read_b64_tr_b16 reads below.
@@ -89,7 +90,16 @@ struct AttnArgs {
     int B, H, Sq, Sk;
     int ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
     float scale;
+    // attention-probability dropout (src/model.py:142): the forward draws the keep bits (Philox,
+    // common.h; row = (b·H + h)·Sq + q, col = key) and stores them, one u64 per (row, 64-key tile), bit
+    // key mod 64 — the backward reads them back.  mbits == nullptr: no dropout.
+    DropSite drop;
+    uint64_t* mbits;
+    int mwords;  // u64 words per row = ceil(Sk / 64)
 };
+
+// Dropout factor of one probability: 1/(1-p) kept, 0 dropped.
+__device__ __forceinline__ float keep_scale(unsigned bits, int j, float scale) { return ((bits >> j) & 1u) ? scale : 0.f; }
 
 constexpr float AT_LOG2E = 1.4426950408889634f;
 
@@ -119,9 +129,13 @@ __device__ __forceinline__ float exp_sc(float s, float c, float shift2) {
 // staged sK / sV tiles): scores, running max / sum update, Oᵀ += Vᵀ·Pᵀ.  m is the running max of the
 // RAW scores (before the 1/sqrt(d) scale).  MASK=false: every key of the tile is valid for every query
 // of the wave.
-template <bool CAUSAL, bool MASK>
+// DROP: P·keep/(1-p) feeds the PV product (the row sum l stays undropped: softmax, then dropout), and
+// the tile's keep bits of this lane's query are OR-combined over its 4 lane rows into *mword (the u64
+// of (row, key tile); written by the g == 0 lanes).
+template <bool CAUSAL, bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int key0, int q, int Sk, float c,
-                                            const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l) {
+                                            const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l,
+                                            const DropSite& drop, int64_t arow, uint64_t* mword) {
     const int g = (threadIdx.x & 63) >> 4;
     f32x4 s[4];
 #pragma unroll
@@ -163,6 +177,27 @@ __device__ __forceinline__ void fwd_kv_tile(const char* sK, const char* sV, int 
     m = mnew;
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    if constexpr (DROP) {
+        uint32_t lo = 0, hi = 0;  // keys key0+0..31 / key0+32..63 of this query
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            const unsigned kb4 = drop_keep4(drop, arow, key0 + kb * 16 + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[kb][r] *= keep_scale(kb4, r, drop.scale);
+            const uint32_t sh = (uint32_t)kb4 << (16 * (kb & 1) + 4 * g);
+            if (kb < 2) lo |= sh;
+            else hi |= sh;
+        }
+        auto r16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        lo = r16[0] | r16[1];
+        r16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        hi = r16[0] | r16[1];
+        auto r32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        lo = r32[0] | r32[1];
+        r32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        hi = r32[0] | r32[1];
+        if (g == 0 && mword) *mword = ((uint64_t)hi << 32) | lo;
+    }
     // Oᵀ[d][q] += Σ_key V[key][d] P[q][key]
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -178,11 +213,19 @@ __device__ __forceinline__ bool tile_masked(int key0, int Sk, int qw0) {
     return key0 + AT_T > Sk || (CAUSAL && key0 + AT_T - 1 > qw0);
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __device__ __forceinline__ void fwd_tile(const char* sK, const char* sV, int key0, int q, int qw0, int Sk, float c,
-                                         const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l) {
-    if (tile_masked<CAUSAL>(key0, Sk, qw0)) fwd_kv_tile<CAUSAL, true>(sK, sV, key0, q, Sk, c, qf, o, m, l);
-    else fwd_kv_tile<CAUSAL, false>(sK, sV, key0, q, Sk, c, qf, o, m, l);
+                                         const bf16x8 (&qf)[2], f32x4 (&o)[4], float& m, float& l,
+                                         const DropSite& drop, int64_t arow, uint64_t* mword) {
+    if (tile_masked<CAUSAL>(key0, Sk, qw0))
+        fwd_kv_tile<CAUSAL, true, DROP>(sK, sV, key0, q, Sk, c, qf, o, m, l, drop, arow, mword);
+    else
+        fwd_kv_tile<CAUSAL, false, DROP>(sK, sV, key0, q, Sk, c, qf, o, m, l, drop, arow, mword);
+}
+
+// Keep bits of (row, key) pairs stored by the forward: u64 word of (row, key tile), bit key mod 64.
+__device__ __forceinline__ float stored_keep(const uint64_t* mrow, int key, float scale) {
+    return ((mrow[key >> 6] >> (key & 63)) & 1ull) ? scale : 0.f;
 }
 
 // Normalised output row (bf16) and the log-sum-exp (natural log, scaled scores) of this lane's query.
@@ -205,10 +248,20 @@ __device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q
 // dK/dV contribution of one 64-query tile (Q, dO, LSE, δ staged) for this lane's key: P recomputed,
 // dS = P∘(dP − δ); dVᵀ += dOᵀ·Pᵀ, dKᵀ += Qᵀ·dSᵀ.  tS (optional): dS also stored key-major, bf16, at
 // tile row krow (the fused short backward reuses it for dQ).  MASK=false: no pair of the tile is masked.
-template <bool CAUSAL, bool MASK>
+// Keep bits of the dropout backward (DROP): mcol points at the u64 word of (query q0, this lane's key
+// tile); word of query q0 + i at mcol[i·mstride], bit kbit = key mod 64.  With dropout P̃ = P·Z
+// (Z = keep/(1-p)) feeds dV, and dS = P∘(dP̃∘Z − δ) (δ = rowsum(dO∘O) is unchanged).
+struct DropBits {
+    const uint64_t* mcol;
+    int mstride, kbit;
+    float scale;
+};
+
+template <bool CAUSAL, bool MASK, bool DROP>
 __device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
                                          int key, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
-                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow) {
+                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow,
+                                         const DropBits& db) {
     const int g = (threadIdx.x & 63) >> 4;
     f32x4 p[4], ds[4];
 #pragma unroll
@@ -229,8 +282,15 @@ __device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const 
                 const bool masked = qq >= Sq || key >= Sk || (CAUSAL && key > qq);
                 pv = masked ? 0.f : pv;
             }
-            p[qb][r] = pv;
-            ds[qb][r] = pv * (dp[r] - sD[ql]);
+            if constexpr (DROP) {
+                const float z = q0 + ql < Sq ? (((db.mcol[(size_t)ql * db.mstride] >> db.kbit) & 1ull) ? db.scale : 0.f)
+                                             : 0.f;
+                p[qb][r] = pv * z;
+                ds[qb][r] = pv * (dp[r] * z - sD[ql]);
+            } else {
+                p[qb][r] = pv;
+                ds[qb][r] = pv * (dp[r] - sD[ql]);
+            }
         }
         if (tS) {  // dS[key][q..q+3] -> key-major LDS tile (one 8-byte store per lane)
             bf16x4 w;
@@ -258,21 +318,23 @@ __device__ __forceinline__ bool dkv_masked(int q0, int Sq, int kw0, int Sk) {
     return q0 + AT_T > Sq || kw0 + 16 > Sk || (CAUSAL && kw0 + 15 > q0);
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __device__ __forceinline__ void dkv_step(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
                                          int key, int kw0, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
-                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow) {
+                                         const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow,
+                                         const DropBits& db) {
     if (dkv_masked<CAUSAL>(q0, Sq, kw0, Sk))
-        dkv_tile<CAUSAL, true>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow);
+        dkv_tile<CAUSAL, true, DROP>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
     else
-        dkv_tile<CAUSAL, false>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow);
+        dkv_tile<CAUSAL, false, DROP>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
 }
 
-// dQ contribution of one 64-key tile for this lane's query (lq2 = LSE·log2e, dl = δ).
-template <bool CAUSAL, bool MASK>
+// dQ contribution of one 64-key tile for this lane's query (lq2 = LSE·log2e, dl = δ).  DROP: mword =
+// the stored keep bits of (this query, this key tile).
+template <bool CAUSAL, bool MASK, bool DROP>
 __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, int key0, int q, int Sq, int Sk, float c,
                                         float lq2, float dl, const bf16x8 (&qf)[2], const bf16x8 (&dof)[2],
-                                        f32x4 (&dq)[4]) {
+                                        f32x4 (&dq)[4], uint64_t mword, float dscale) {
     const int g = (threadIdx.x & 63) >> 4;
     f32x4 ds[4];
 #pragma unroll
@@ -291,7 +353,12 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, int key0
                 const bool masked = key >= Sk || q >= Sq || (CAUSAL && key > q);
                 pv = masked ? 0.f : pv;
             }
-            ds[kb][r] = pv * (dp[r] - dl);
+            if constexpr (DROP) {
+                const float z = ((mword >> (kb * 16 + 4 * g + r)) & 1ull) ? dscale : 0.f;
+                ds[kb][r] = pv * (dp[r] * z - dl);
+            } else {
+                ds[kb][r] = pv * (dp[r] - dl);
+            }
         }
     }
 #pragma unroll
@@ -346,8 +413,8 @@ __device__ __forceinline__ void ring_sync(int after) {
     __builtin_amdgcn_s_barrier();
 }
 
-template <bool CAUSAL, int NS>
-__global__ __launch_bounds__(256, 4) void attn_fwd_kernel(AttnArgs a) {
+template <bool CAUSAL, int NS, bool DROP>
+__global__ __launch_bounds__(256, DROP ? 3 : 4) void attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) char ring[NS * 2 * AT_TILE_BYTES];  // [stage][K|V]
     const AttnBlock blk = attn_block();
     const int b = blk.b, h = blk.h;
@@ -382,12 +449,15 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_kernel(AttnArgs a) {
         AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
         AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
     };
+    const int64_t arow = ((int64_t)b * a.H + h) * a.Sq + q;  // dropout row of this lane's query
+    uint64_t* mrow = DROP && q < a.Sq ? a.mbits + arow * a.mwords : nullptr;
     for (int s = 0; s < NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
         ring_sync<4, NS>(min(NS - 2, nkt - 1 - kt));
         if (kt + NS - 1 < nkt) issue(kt + NS - 1);
         const char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
-        fwd_tile<CAUSAL>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l);
+        fwd_tile<CAUSAL, DROP>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l, a.drop,
+                               arow, mrow ? mrow + kt : nullptr);
     }
     fwd_store(a, b, h, q, o, m, l);
 }
@@ -422,8 +492,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
 
 // dK, dV: workgroup = 64 keys of one (b, h), each wave 16 keys; loop over query tiles.  A ring stage holds
 // the Q and dO tiles and the tile's 64 LSE and δ values (one 256-B DMA per wave: waves 0/2 LSE, 1/3 δ).
-template <bool CAUSAL, int NS>
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkv_kernel(AttnArgs a) {
+template <bool CAUSAL, int NS, bool DROP>
+__global__ __launch_bounds__(256, DROP ? 2 : 3) void attn_bwd_dkv_kernel(AttnArgs a) {
     constexpr int STAGE = 2 * AT_TILE_BYTES + 4 * AT_T * 4;
     __shared__ __attribute__((aligned(16))) char ring[NS * STAGE];
     const AttnBlock blk = attn_block();
@@ -463,7 +533,17 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_kernel(AttnArgs a) {
         glds4(rowv + min(q0 + lane, a.Sq - 1),
               __builtin_amdgcn_readfirstlane(lds_addr_of(st + 2 * AT_TILE_BYTES + wave * AT_T * 4)));
     };
+    // dropout keep bits of this workgroup's key tile for every query (u64 per query), staged in LDS
+    // before the ring starts (a plain load inside the loop would make the compiler drain the untracked
+    // LDS-DMA ring at every use)
+    __shared__ uint64_t smask[DROP ? AT_MAX_SQ_DROP : 1];
+    if constexpr (DROP) {
+        const uint64_t* src = a.mbits + ((size_t)b * a.H + h) * a.Sq * a.mwords + blk.x;
+        for (int i = threadIdx.x; i < a.Sq; i += 256) smask[i] = src[(size_t)i * a.mwords];
+        __syncthreads();
+    }
     for (int s = 0; s < NS - 1 && s < n; ++s) issue(s);
+    DropBits db{nullptr, 1, key & 63, a.drop.scale};
     for (int i = 0; i < n; ++i) {
         ring_sync<5, NS>(min(NS - 2, n - 1 - i));
         if (i + NS - 1 < n) issue(i + NS - 1);
@@ -471,8 +551,9 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_kernel(AttnArgs a) {
         const char* sdO = sQ + AT_TILE_BYTES;
         const float* sL = reinterpret_cast<const float*>(sQ + 2 * AT_TILE_BYTES);
         const float* sD = sL + AT_T;
-        dkv_step<CAUSAL>(sQ, sdO, sL, sD, (qt0 + i) * AT_T, key, kblk + wave * 16, a.Sq, a.Sk, c, kf, vf, dk, dv,
-                         nullptr, 0);
+        if (DROP) db.mcol = smask + (qt0 + i) * AT_T;
+        dkv_step<CAUSAL, DROP>(sQ, sdO, sL, sD, (qt0 + i) * AT_T, key, kblk + wave * 16, a.Sq, a.Sk, c, kf, vf, dk, dv,
+                               nullptr, 0, db);
     }
     if (key < a.Sk) {
         size_t tok = (size_t)b * a.Sk + key;
@@ -491,7 +572,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_kernel(AttnArgs a) {
 }
 
 // dQ: workgroup = 64 queries, each wave 16 queries; loop over key tiles (K, V through the ring).
-template <bool CAUSAL, int NS>
+template <bool CAUSAL, int NS, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) char ring[NS * 2 * AT_TILE_BYTES];
     const AttnBlock blk = attn_block();
@@ -530,6 +611,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
         AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
     };
+    // dropout keep bits of the workgroup's 64 queries (mwords u64 each), staged in LDS before the ring
+    __shared__ uint64_t smask[DROP ? AT_MAX_SQ_DROP : 1];
+    if constexpr (DROP) {
+        const uint64_t* src = a.mbits + (((size_t)b * a.H + h) * a.Sq + qblk) * a.mwords;
+        const int nw = (min(a.Sq, qblk + AT_T) - qblk) * a.mwords;
+        for (int i = threadIdx.x; i < nw; i += 256) smask[i] = src[i];
+        __syncthreads();
+    }
     for (int s = 0; s < NS - 1 && s < nkt; ++s) issue(s);
     for (int kt = 0; kt < nkt; ++kt) {
         ring_sync<4, NS>(min(NS - 2, nkt - 1 - kt));
@@ -537,10 +626,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         const char* sK = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         const char* sV = sK + AT_TILE_BYTES;
         const int key0 = kt * AT_T;
+        const uint64_t mw = DROP && q < a.Sq ? smask[(q - qblk) * a.mwords + kt] : 0ull;
         if (tile_masked<CAUSAL>(key0, a.Sk, qblk + wave * 16) || qblk + wave * 16 + 16 > a.Sq)
-            dq_tile<CAUSAL, true>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq);
+            dq_tile<CAUSAL, true, DROP>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq, mw, a.drop.scale);
         else
-            dq_tile<CAUSAL, false>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq);
+            dq_tile<CAUSAL, false, DROP>(sK, sV, key0, q, a.Sq, a.Sk, c, lq2, dq_delta, qf, dof, dq, mw, a.drop.scale);
     }
     if (q < a.Sq) {
         __bf16* out = a.dq + ((size_t)b * a.Sq + q) * a.lddq + h * AT_D;
@@ -563,7 +653,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 constexpr int AS_MAX = 128;                          // max Sq / Sk of the fused path
 constexpr int AS_TILES = AS_MAX / AT_T;              // 64-row tiles per operand
 constexpr int AS_OPER = AS_TILES * AT_TILE_BYTES;    // 16 KiB per staged operand
-constexpr int AS_LDS = 4 * AS_OPER + AS_TILES * AS_TILES * AT_TILE_BYTES + 2 * AS_MAX * 4;  // 96 KiB + 1 KiB
+// + the dropout keep bits of the (b, h): [query][AS_TILES] u64
+constexpr int AS_LDS = 4 * AS_OPER + AS_TILES * AS_TILES * AT_TILE_BYTES + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
 
 // 128 rows x 64 dims of a token-major operand as two swizzled 64-row tiles (rows >= nrows are zero):
 // the loads are issued first (2 x 16 B per thread), then written to LDS, so several staged operands
@@ -588,7 +679,7 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
     }
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sQ = smem;
@@ -598,6 +689,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     char* sdS = sV + AS_OPER;                          // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
     float* sL = reinterpret_cast<float*>(sdS + AS_TILES * AS_TILES * AT_TILE_BYTES);
     float* sD = sL + AS_MAX;
+    uint64_t* sM = reinterpret_cast<uint64_t*>(sD + AS_MAX);  // dropout keep bits [query][AS_TILES]
     const int b = blockIdx.z, h = blockIdx.y;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i16 = lane & 15, g = lane >> 4;
@@ -610,6 +702,11 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         const Rows128 rdo = load_rows(dOb, a.lddo, a.Sq);
         const Rows128 rk = load_rows(Kb, a.ldk, a.Sk);
         const Rows128 rv = load_rows(Vb, a.ldv, a.Sk);
+        uint64_t mv = 0;  // one keep-bit word per thread (Sq * AS_TILES <= 256 < 512 threads)
+        if constexpr (DROP) {
+            const int qq = threadIdx.x / AS_TILES, w = threadIdx.x % AS_TILES;
+            if (qq < a.Sq && w < a.mwords) mv = a.mbits[(((size_t)b * a.H + h) * a.Sq + qq) * a.mwords + w];
+        }
         // δ[q] = Σ_d dO·O (4 threads per query, 16 dims each) and the forward LSE
         const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
         bf16x8 x0, x1, y0, y1;
@@ -627,6 +724,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         put_rows(sdO, rdo);
         put_rows(sK, rk);
         put_rows(sV, rv);
+        if (DROP && threadIdx.x < AS_MAX * AS_TILES) sM[threadIdx.x] = mv;
         float dsum = 0.f;
         if (ql < a.Sq) {
 #pragma unroll
@@ -661,12 +759,14 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
             dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         const int nqt = (a.Sq + AT_T - 1) / AT_T;
+        DropBits db{nullptr, AS_TILES, key & 63, a.drop.scale};
         for (int qt = CAUSAL ? kt : 0; qt < nqt; ++qt) {
             const char* tQ = sQ + qt * AT_TILE_BYTES;
             const char* tdO = sdO + qt * AT_TILE_BYTES;
             char* tS = sdS + (kt * AS_TILES + qt) * AT_TILE_BYTES;
-            dkv_step<CAUSAL>(tQ, tdO, sL + qt * AT_T, sD + qt * AT_T, qt * AT_T, key, wave * 16, a.Sq, a.Sk, c, kf, vf,
-                             dk, dv, tS, krow);
+            if (DROP) db.mcol = sM + qt * AT_T * AS_TILES + kt;
+            dkv_step<CAUSAL, DROP>(tQ, tdO, sL + qt * AT_T, sD + qt * AT_T, qt * AT_T, key, wave * 16, a.Sq, a.Sk, c, kf,
+                                   vf, dk, dv, tS, krow, db);
         }
         if (key < a.Sk) {
             size_t tok = (size_t)b * a.Sk + key;
@@ -739,27 +839,38 @@ bool g_attn_generic = false;  // ergm_attn_tune: force the tiled kernels even fo
 // initial value (A/B runs inside the step)
 int g_attn_ns = getenv("ERGM_ATTN_NS") ? atoi(getenv("ERGM_ATTN_NS")) : 0;
 
-template <bool CAUSAL, int NS>
+template <bool CAUSAL, int NS, bool DROP>
 void launch_tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
-    hipLaunchKernelGGL((attn_fwd_kernel<CAUSAL, NS>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<CAUSAL, NS, DROP>), grid, dim3(256), 0, s, a);
 }
 // Defaults: 2 stages everywhere (tools/attn_bench.py at the C4 shape: forward fastest at 2, the dK/dV
 // kernel then fits 3 waves per SIMD without spills; dQ 3 isolated, 2 inside the C4 step, #20).
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 void tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
-    if (g_attn_ns == 3) launch_tiled_fwd<CAUSAL, 3>(grid, s, a);
-    else if (g_attn_ns == 4) launch_tiled_fwd<CAUSAL, 4>(grid, s, a);
-    else launch_tiled_fwd<CAUSAL, 2>(grid, s, a);
+    if (g_attn_ns == 3) launch_tiled_fwd<CAUSAL, 3, DROP>(grid, s, a);
+    else if (g_attn_ns == 4) launch_tiled_fwd<CAUSAL, 4, DROP>(grid, s, a);
+    else launch_tiled_fwd<CAUSAL, 2, DROP>(grid, s, a);
 }
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 void tiled_bwd(dim3 gk, dim3 gq, hipStream_t s, const AttnArgs& a) {
     const int ns_kv = g_attn_ns ? g_attn_ns : 2, ns_q = g_attn_ns ? g_attn_ns : 2;
-    if (ns_kv == 3) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 3>), gk, dim3(256), 0, s, a);
-    else if (ns_kv == 4) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 4>), gk, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 2>), gk, dim3(256), 0, s, a);
-    if (ns_q == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 2>), gq, dim3(256), 0, s, a);
-    else if (ns_q == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 4>), gq, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 3>), gq, dim3(256), 0, s, a);
+    if (ns_kv == 3) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 3, DROP>), gk, dim3(256), 0, s, a);
+    else if (ns_kv == 4) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 4, DROP>), gk, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 2, DROP>), gk, dim3(256), 0, s, a);
+    if (ns_q == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 2, DROP>), gq, dim3(256), 0, s, a);
+    else if (ns_q == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 4, DROP>), gq, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 3, DROP>), gq, dim3(256), 0, s, a);
+}
+// Dropout fields of AttnArgs from the C-ABI descriptor (rows (b·H + h)·Sq + q, cols Sk).
+int set_drop(AttnArgs& a, const ergm_dropout* d, void* keep_bits) {
+    ERGM_TRY(check_dropout(d));
+    a.drop = drop_site_of(d, a.Sk);
+    a.mwords = (a.Sk + 63) / 64;
+    a.mbits = a.drop.thresh ? reinterpret_cast<uint64_t*>(keep_bits) : nullptr;
+    ERGM_CHECK_ARG(!a.drop.thresh || keep_bits, "attn: dropout needs the keep-bit buffer");
+    ERGM_CHECK_ARG(!a.drop.thresh || (a.Sq <= AT_MAX_SQ_DROP && a.Sk <= AT_MAX_SQ_DROP),
+                   "attn: dropout supports Sq, Sk <= %d", AT_MAX_SQ_DROP);
+    return ERGM_OK;
 }
 }
 
@@ -772,7 +883,8 @@ extern "C" int ergm_attn_tune(int force_generic) {
 }
 
 extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
-                             int Sk, int ldq, int ldk, int ldv, int ldo, int causal, void* stream) {
+                             int Sk, int ldq, int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout,
+                             void* keep_bits, void* stream) {
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && lse && ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd: bad output");
     AttnArgs a{};
@@ -781,19 +893,21 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
     a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
     a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
     a.scale = 0.125f;  // 1/sqrt(64): exact, so x*scale == x / 8.0 (src/model.py:122-125)
+    ERGM_TRY(set_drop(a, dropout, keep_bits));
     hipStream_t s = as_stream(stream);
     // every length takes the tiled kernel: at S = 128 its 2x more workgroups beat the one-workgroup-per-
     // (b, h) form inside the concurrent step (C2 +1.6 %, C5 +0.4 %; profiles/r01_overlap_experiments.txt #19)
     dim3 grid(cdiv(Sq, AT_T), H, B);
-    if (causal) tiled_fwd<true>(grid, s, a);
-    else tiled_fwd<false>(grid, s, a);
+    const bool drop = a.mbits != nullptr;
+    if (causal) drop ? tiled_fwd<true, true>(grid, s, a) : tiled_fwd<true, false>(grid, s, a);
+    else drop ? tiled_fwd<false, true>(grid, s, a) : tiled_fwd<false, false>(grid, s, a);
     return check_launch("attn_fwd");
 }
 
 extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                              const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
-                             int causal, void* stream) {
+                             int causal, const ergm_dropout* dropout, const void* keep_bits, void* stream) {
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && dout && lse && delta && dq && dk && dv, "attn_bwd: null argument");
     ERGM_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 4 == 0 && lddk % 4 == 0 && lddv % 4 == 0,
@@ -808,25 +922,34 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
     a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo;
     a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
     a.scale = 0.125f;
+    ERGM_TRY(set_drop(a, dropout, const_cast<void*>(keep_bits)));
+    const bool drop = a.mbits != nullptr;
     hipStream_t s = as_stream(stream);
     if (Sq <= AS_MAX && Sk <= AS_MAX && !g_attn_generic) {
         static bool attr_set = false;  // benign race: idempotent attribute writes
         if (!attr_set) {
-            if (hipFuncSetAttribute((const void*)attn_bwd_short_kernel<true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess ||
-                hipFuncSetAttribute((const void*)attn_bwd_short_kernel<false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess)
-                return fail(ERGM_EHIP, "attn_bwd: cannot raise dynamic LDS limit");
+            const void* ks[4] = {(const void*)attn_bwd_short_kernel<true, false>,
+                                 (const void*)attn_bwd_short_kernel<false, false>,
+                                 (const void*)attn_bwd_short_kernel<true, true>,
+                                 (const void*)attn_bwd_short_kernel<false, true>};
+            for (const void* k : ks)
+                if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess)
+                    return fail(ERGM_EHIP, "attn_bwd: cannot raise dynamic LDS limit");
             attr_set = true;
         }
         dim3 grid(1, H, B);
-        if (causal) hipLaunchKernelGGL(attn_bwd_short_kernel<true>, grid, dim3(512), AS_LDS, s, a);
-        else hipLaunchKernelGGL(attn_bwd_short_kernel<false>, grid, dim3(512), AS_LDS, s, a);
+        if (causal) {
+            if (drop) hipLaunchKernelGGL((attn_bwd_short_kernel<true, true>), grid, dim3(512), AS_LDS, s, a);
+            else hipLaunchKernelGGL((attn_bwd_short_kernel<true, false>), grid, dim3(512), AS_LDS, s, a);
+        } else {
+            if (drop) hipLaunchKernelGGL((attn_bwd_short_kernel<false, true>), grid, dim3(512), AS_LDS, s, a);
+            else hipLaunchKernelGGL((attn_bwd_short_kernel<false, false>), grid, dim3(512), AS_LDS, s, a);
+        }
         return check_launch("attn_bwd");
     }
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
     hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(B * Sq * H * 4, 256)), dim3(256), 0, s, a);
-    if (causal) tiled_bwd<true>(gk, gq, s, a);
-    else tiled_bwd<false>(gk, gq, s, a);
+    if (causal) drop ? tiled_bwd<true, true>(gk, gq, s, a) : tiled_bwd<true, false>(gk, gq, s, a);
+    else drop ? tiled_bwd<false, true>(gk, gq, s, a) : tiled_bwd<false, false>(gk, gq, s, a);
     return check_launch("attn_bwd");
 }

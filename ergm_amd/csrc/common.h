@@ -97,4 +97,50 @@ __device__ __forceinline__ float gelu_new_grad(float x) {
     return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * 0.044715f * x2);
 }
 
+// ---- dropout (nn.Dropout at src/model.py:142,245,266,506) -------------------------------------
+// Counter-based: the keep decision of element (row, col) of dropout site `site` in forward number
+// `offset` is a pure function of (seed, offset, site, global row, col), so the backward recomputes
+// it instead of storing it.  Random words: Philox4x32-10 (Salmon et al., SC'11; Random123), one call
+// per group of 4 consecutive columns: counter = {g_lo, g_hi, site, offset} with
+// g = row·ceil(cols/4) + col/4, key = seed; element col uses word col & 3.  Dropped iff word < thresh
+// (thresh = round(p·2^32)); kept elements are scaled by 1/(1-p) as torch's dropout does.
+struct DropSite {
+    uint32_t key0, key1;  // seed
+    uint32_t site;        // counter word 2: which nn.Dropout (ergm_hip.h ERGM_DROP_SITE_*)
+    uint32_t offset;      // counter word 3: forward number
+    uint32_t thresh;      // 0: dropout off
+    float scale;          // 1 / (1 - p)
+    int64_t row0;         // global row of the caller's row 0 (DP ranks / batch-half chains)
+    int64_t cols4;        // ceil(cols / 4): counter groups per row
+};
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Keep bits of columns col..col+3 (col % 4 == 0) of `row` (caller-relative): bit j = column col+j kept.
+__device__ __forceinline__ unsigned drop_keep4(const DropSite& d, int64_t row, int col) {
+    const uint64_t g = (uint64_t)(d.row0 + row) * (uint64_t)d.cols4 + (uint64_t)(col >> 2);
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)g, (uint32_t)(g >> 32), d.site, d.offset), d.key0, d.key1);
+    return (r.x >= d.thresh ? 1u : 0u) | (r.y >= d.thresh ? 2u : 0u) | (r.z >= d.thresh ? 4u : 0u) |
+           (r.w >= d.thresh ? 8u : 0u);
+}
+// Single element (any col): the word col & 3 of its group.
+__device__ __forceinline__ bool drop_keep1(const DropSite& d, int64_t row, int col) {
+    return (drop_keep4(d, row, col & ~3) >> (col & 3)) & 1u;
+}
+
+// Host: the descriptor of one site (p in [0, 1); p == 0 gives thresh 0 = off).
+DropSite make_drop_site(uint64_t seed, uint32_t offset, uint32_t site, float p, int64_t row0, int64_t cols);
+DropSite drop_site_of(const ergm_dropout* d, int64_t cols);  // NULL or p == 0: off
+int check_dropout(const ergm_dropout* d);
+int dropout_apply_f32(const DropSite& d, float* x, int rows, int cols, int ld, hipStream_t s);
+
 }  // namespace ergm

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const float* __restrict__ wpe, const float* __restrict__ vis,
                                                         int ld_vis, const float* __restrict__ aud,
                                                         float* __restrict__ h0, __bf16* __restrict__ cap, int ld_cap,
-                                                        int B, int S, int E, int V) {
+                                                        int B, int S, int E, int V, DropSite drop) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + wave;
     if (t >= B * S) return;
@@ -45,6 +45,13 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
         if (ok_ty) {
             float4 y = *reinterpret_cast<const float4*>(wte + (size_t)ty * E + c);
             x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+        }
+        if (drop.thresh) {  // self.drop(hidden_states), src/model.py:506
+            const unsigned k = drop_keep4(drop, t, c);
+            x.x = (k & 1u) ? x.x * drop.scale : 0.f;
+            x.y = (k & 2u) ? x.y * drop.scale : 0.f;
+            x.z = (k & 4u) ? x.z * drop.scale : 0.f;
+            x.w = (k & 8u) ? x.w * drop.scale : 0.f;
         }
         *reinterpret_cast<float4*>(h0 + (size_t)t * E + c) = x;
         float4 cv = ok_c ? *reinterpret_cast<const float4*>(wte + (size_t)cid * E + c) : make_float4(0, 0, 0, 0);
@@ -301,7 +308,7 @@ using namespace ergm;
 namespace ergm {
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
-                 int V, hipStream_t s) {
+                 int V, hipStream_t s, const DropSite& drop) {
     ERGM_CHECK_ARG(ids && cap_ids && wte && wpe && h0 && cap, "embed_fwd: null argument");
     ERGM_CHECK_ARG(B > 0 && S > 0 && E > 0 && E % 4 == 0 && E <= 1024 && V > 0, "embed_fwd: bad shape");
     ERGM_CHECK_ARG((vis == nullptr) == (aud == nullptr), "embed_fwd: visual and audio features go together");
@@ -311,10 +318,10 @@ int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, 
     ERGM_CHECK_ARG(ld_cap >= E && ld_cap % 4 == 0, "embed_fwd: bad ld_cap");
     auto* cb = reinterpret_cast<__bf16*>(cap);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
-        case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
-        case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
-        default: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V); break;
+        case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        default: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
     }
     return check_launch("embed_fwd");
 }
@@ -322,8 +329,10 @@ int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, 
 
 extern "C" int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
                               const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0, void* cap,
-                              int B, int S, int E, int V, void* stream) {
-    return embed_fwd_ld(ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cap, E, B, S, E, V, as_stream(stream));
+                              int B, int S, int E, int V, const ergm_dropout* dropout, void* stream) {
+    ERGM_TRY(check_dropout(dropout));
+    return embed_fwd_ld(ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cap, E, B, S, E, V, as_stream(stream),
+                        drop_site_of(dropout, E));
 }
 
 namespace ergm {

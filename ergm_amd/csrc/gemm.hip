@@ -42,6 +42,7 @@ struct GemmArgs {
     const float* a_scale;  // fp8 GEMM: per-row dequantisation scale of A [M] (nullptr: none)
     const float* b_scale;  // fp8 GEMM: per-column dequantisation scale of B [N]
     int nt_store;          // C written with non-temporal stores (streamed output)
+    DropSite drop;         // BIAS_RESID: dropout of the residual branch (src/model.py:245,266), rows m, cols n
 };
 
 template <int EPI, bool OUT_BF16>
@@ -54,6 +55,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
         reinterpret_cast<__bf16*>(a.aux_out)[(size_t)m * a.ld_aux_out + n] = pre;
         v = gelu_new(v);
     } else if (EPI == ERGM_EPI_BIAS_RESID) {
+        if (a.drop.thresh) v = drop_keep1(a.drop, m, n) ? v * a.drop.scale : 0.f;
         v += reinterpret_cast<const float*>(a.aux)[(size_t)m * a.ld_aux + n];
     } else if (EPI == ERGM_EPI_GELU_BWD) {
         float x = bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);
@@ -89,6 +91,11 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
         }
         *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.aux_out) + (size_t)m * a.ld_aux_out + n) = pre;
     } else if (EPI == ERGM_EPI_BIAS_RESID) {
+        if (a.drop.thresh) {  // residual-branch dropout, then the residual add
+            const unsigned k = drop_keep4(a.drop, m, n) | (drop_keep4(a.drop, m, n + 4) << 4);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ((k >> j) & 1u) ? v[j] * a.drop.scale : 0.f;
+        }
         const float* r = reinterpret_cast<const float*>(a.aux) + (size_t)m * a.ld_aux + n;
         float4 r0 = *reinterpret_cast<const float4*>(r), r1 = *reinterpret_cast<const float4*>(r + 4);
         v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
@@ -955,6 +962,10 @@ extern "C" int ergm_gemm_f8(const ergm_gemm_desc* d, const void* A, const float*
     a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
     a.a_scale = a_scale;
     a.b_scale = b_scale;
+    ERGM_TRY(check_dropout(d->dropout));
+    ERGM_CHECK_ARG(!d->dropout || d->dropout->p == 0.f || e == ERGM_EPI_BIAS_RESID,
+                   "ergm_gemm_f8: dropout applies to the BIAS_RESID epilogue only");
+    a.drop = drop_site_of(d->dropout, d->N);
     hipStream_t s = as_stream(stream);
     const bool ob = d->c_dtype == ERGM_BF16;
     switch (e) {
@@ -1041,6 +1052,9 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
                    "ergm_gemm: residual/accumulate epilogues need f32 C");
     ERGM_CHECK_ARG(!(e == ERGM_EPI_BIAS_RESID || e == ERGM_EPI_GELU_BWD) || d->aux, "ergm_gemm: epilogue needs aux");
     ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || d->aux_out, "ergm_gemm: BIAS_GELU needs aux_out");
+    ERGM_TRY(check_dropout(d->dropout));
+    ERGM_CHECK_ARG(!d->dropout || d->dropout->p == 0.f || e == ERGM_EPI_BIAS_RESID,
+                   "ergm_gemm: dropout applies to the BIAS_RESID epilogue only");
 
     trace_shape(d);
     GemmPlan p = plan_gemm(d);
@@ -1059,6 +1073,7 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     a.k_per_split = p.kps;
     a.slab = nullptr;
     a.a_scale = a.b_scale = nullptr;
+    a.drop = drop_site_of(d->dropout, d->N);
     // the vocabulary-wide bf16 logits (206 MB at C2) are streamed out with non-temporal stores so they
     // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
     // profiles/r01_overlap_experiments.txt #14); ERGM_NT_STORE=0 disables (A/B)

@@ -32,14 +32,15 @@ int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
-                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s);
+                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
+                       const DropSite& drop);
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
                              float* const* dgamma, float* const* dbeta, hipStream_t s);
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
-                 int V, hipStream_t s);
+                 int V, hipStream_t s, const DropSite& drop);
 int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, int T, int V, uint64_t* keys,
                    uint8_t* row_flag, int n_flag, hipStream_t s);
 int embed_sort_capacity(int T);
@@ -140,9 +141,18 @@ struct ergm_model_plan {
     // inputs
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
     const float *vis, *aud;
-    const int* n_valid;
-    int B_global;
+    const int* n_valid;  // [0] valid LM labels, [1] valid emotion labels (global under DP)
     bool have_fwd;
+    // dropout (src/model.py:142,245,266,506): probabilities, seed and forward number set by the caller
+    // (ergm_model_set_dropout) for the next training forward; `drop_on` is latched by that forward and
+    // read by its backward.  abits: the attention forwards' keep bits, [2L][B·H·S][mwords] u64.
+    float p_attn, p_resid, p_embd;
+    uint64_t drop_seed;
+    uint32_t drop_offset;
+    int b_base;  // global batch index of local sample 0 (data-parallel rank offset)
+    bool drop_on;
+    uint64_t* abits;
+    int mwords;
     // kernel probe (bench timing)
     int probe;
     hipEvent_t ev_begin, ev_end;
@@ -237,6 +247,8 @@ size_t carve(ergm_model_plan* P, char* base) {
         P->dproj = nullptr;
     }
     P->keys = c.take<uint64_t>(embed_sort_capacity(T));
+    P->mwords = (d.seq + 63) / 64;
+    P->abits = c.take<uint64_t>((size_t)2 * L * BHS * P->mwords);
     P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
     P->d_o = c.take<__bf16>(T * E);
@@ -265,15 +277,41 @@ inline int ws_need(ergm_model_plan* P, size_t bytes) {
     return ERGM_OK;
 }
 
+// Dropout descriptor of `site` for rows starting at global row `row0` (p == 0: off).  The residual
+// sites count token rows ((b_base + b)·S + s), the attention sites (b·H + h)·S + q rows.
+ergm_dropout drop_desc(const ergm_model_plan* P, uint32_t site, float p, int64_t row0) {
+    ergm_dropout d{};
+    d.seed = P->drop_seed;
+    d.offset = P->drop_offset;
+    d.site = site;
+    d.p = P->drop_on ? p : 0.f;
+    d.row0 = row0;
+    return d;
+}
+ergm_dropout resid_drop(const ergm_model_plan* P, int resid_index, int b0) {
+    return drop_desc(P, (uint32_t)resid_index, resid_index == 0 ? P->p_embd : P->p_resid,
+                     (int64_t)(P->b_base + b0) * P->d.seq);
+}
+ergm_dropout attn_drop(const ergm_model_plan* P, int l, int cross, int b0) {
+    return drop_desc(P, ERGM_DROP_SITE_ATTN(P->d.n_layer, l, cross), P->p_attn,
+                     (int64_t)(P->b_base + b0) * P->d.n_head * P->d.seq);
+}
+uint64_t* attn_bits(const ergm_model_plan* P, int l, int cross, int b0) {
+    if (P->dry) return nullptr;
+    const size_t per = (size_t)P->d.batch * P->d.n_head * P->d.seq * P->mwords;
+    return P->abits + (2 * (size_t)l + cross) * per + (size_t)b0 * P->d.n_head * P->d.seq * P->mwords;
+}
+
 int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, int lda, int al, const void* B,
          int ldb, int bl, void* C, int ldc, int cdt, int epi, const float* bias = nullptr, const void* aux = nullptr,
-         int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const float* alpha_dev = nullptr) {
+         int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const float* alpha_dev = nullptr,
+         const ergm_dropout* dropout = nullptr) {
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
     g.a_layout = al; g.b_layout = bl; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
-    g.split_k = 0; g.alpha_dev = alpha_dev;
+    g.split_k = 0; g.alpha_dev = alpha_dev; g.dropout = dropout;
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
@@ -284,13 +322,14 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
 // fp8 forward GEMM: C[M][N] = epi(sa[m]·sb[n]·A8[m][:]·B8t[n][:]) (both operands k-contiguous, K bytes)
 int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* Bt,
           const float* sb, void* C, int ldc, int cdt, int epi, const float* bias, const void* aux = nullptr,
-          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0) {
+          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const ergm_dropout* dropout = nullptr) {
     if (P->dry) return ERGM_OK;
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
     g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = ldc;
     g.a_layout = ERGM_MK; g.b_layout = ERGM_NK; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
+    g.dropout = dropout;
     return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
 }
 
@@ -346,7 +385,10 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
     const int T = P->T, E = P->d.n_embd;
     float* pg = P->ln_part[slot];
     float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
-    ERGM_TRY(layernorm_bwd_main(P->dy, x, mean, rstd, gamma, P->dh, dh_b, pg, pb, T, E, s));
+    // dh_b feeds the residual branch that produced this residual-stream tensor (slot = its index):
+    // through that branch's dropout (slot 0, the embeddings: unused by any GEMM)
+    const ergm_dropout dd = resid_drop(P, slot, 0);
+    ERGM_TRY(layernorm_bwd_main(P->dy, x, mean, rstd, gamma, P->dh, dh_b, pg, pb, T, E, s, drop_site_of(&dd, E)));
     ERGM_CHECK_ARG(P->ln_pending < 4, "model: too many pending LayerNorm reductions");
     const int k = P->ln_pending++;
     P->lnr_pg[k] = pg; P->lnr_pb[k] = pb; P->lnr_dg[k] = dgamma; P->lnr_db[k] = dbeta;
@@ -413,7 +455,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s);
 
 extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     if (!dims) return 0;
-    ergm_model_plan P;
+    ergm_model_plan P{};
     P.d = *dims;
     memset(&P.p, 0, sizeof(P.p));
     P.T = dims->batch * dims->seq;
@@ -526,9 +568,13 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->row_pos = nullptr;
     P->lookup_compact = nullptr;
     P->n_valid = nullptr;
-    P->B_global = d.batch;
     P->probe = 0;
     P->ev_begin = P->ev_end = nullptr;
+    P->p_attn = P->p_resid = P->p_embd = 0.f;
+    P->drop_seed = 0;
+    P->drop_offset = 0;
+    P->b_base = 0;
+    P->drop_on = false;
     *out = P;
     return ERGM_OK;
 }
@@ -558,6 +604,22 @@ extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begi
     P->probe = probe;
     P->ev_begin = reinterpret_cast<hipEvent_t>(ev_begin);
     P->ev_end = reinterpret_cast<hipEvent_t>(ev_end);
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_dropout(ergm_model_plan* P, float attn_p, float resid_p, float embd_p, uint64_t seed,
+                                      uint32_t offset, int batch_base) {
+    ERGM_CHECK_ARG(P, "model_set_dropout: null plan");
+    ERGM_CHECK_ARG(attn_p >= 0.f && attn_p < 1.f && resid_p >= 0.f && resid_p < 1.f && embd_p >= 0.f && embd_p < 1.f,
+                   "model_set_dropout: probabilities must be in [0, 1)");
+    ERGM_CHECK_ARG(batch_base >= 0, "model_set_dropout: batch_base must be >= 0");
+    ERGM_CHECK_ARG(attn_p == 0.f || P->d.seq <= 1024, "model_set_dropout: attention dropout needs seq <= 1024");
+    P->p_attn = attn_p;
+    P->p_resid = resid_p;
+    P->p_embd = embd_p;
+    P->drop_seed = seed;
+    P->drop_offset = offset;
+    P->b_base = batch_base;
     return ERGM_OK;
 }
 
@@ -592,15 +654,13 @@ extern "C" int ergm_model_set_lookup_compact(ergm_model_plan* P, const int* row_
 
 extern "C" int ergm_model_set_inputs(ergm_model_plan* P, const int64_t* ids, const int64_t* tt,
                                      const int64_t* cap_ids, const float* vis, const float* aud,
-                                     const int64_t* labels, const int64_t* emotion_labels, const int* n_valid_global,
-                                     int B_global) {
+                                     const int64_t* labels, const int64_t* emotion_labels, const int* counts_global) {
     ERGM_CHECK_ARG(P && ids && cap_ids, "model_set_inputs: input_ids and caption_ids are required");
     ERGM_CHECK_ARG((vis == nullptr) == (aud == nullptr), "model_set_inputs: visual/audio features go together");
     ERGM_CHECK_ARG(!vis || P->d.has_features, "model_set_inputs: plan built without features");
-    ERGM_CHECK_ARG(!labels || n_valid_global, "model_set_inputs: labels need n_valid_global");
+    ERGM_CHECK_ARG(!(labels || emotion_labels) || counts_global, "model_set_inputs: labels need counts_global");
     P->ids = ids; P->tt = tt; P->cap_ids = cap_ids; P->vis = vis; P->aud = aud;
-    P->labels = labels; P->emo_labels = emotion_labels; P->n_valid = n_valid_global;
-    P->B_global = B_global > 0 ? B_global : P->d.batch;
+    P->labels = labels; P->emo_labels = emotion_labels; P->n_valid = counts_global;
     return ERGM_OK;
 }
 
@@ -637,6 +697,11 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
     float* sa = f8 && !P->dry ? P->sa + r0 : nullptr;
     float* sf = f8 && !P->dry ? P->sf + r0 : nullptr;
     if (w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
+    // dropout sites of this block over the chain's rows (src/model.py:142 probabilities, :245 / :266
+    // residual branches)
+    const ergm_dropout dr_attn = resid_drop(P, 3 * l + 1, b0), dr_cross = resid_drop(P, 3 * l + 2, b0),
+                       dr_mlp = resid_drop(P, 3 * l + 3, b0);
+    const ergm_dropout dp_self = attn_drop(P, l, 0, b0), dp_cross = attn_drop(P, l, 1, b0);
     // self-attention sub-block (src/model.py:297-309)
     if (!P->dry)
         ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
@@ -649,14 +714,14 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
                       ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
     if (!P->dry)
         ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, nb, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
-                               s));
+                               &dp_self, attn_bits(P, l, 0, b0), s));
     if (f8) {
         if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
         ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, &dr_attn));
     } else {
         ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E));
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, nullptr, &dr_attn));
     }
     // cross-attention over caption embeddings (src/model.py:311-329)
     if (!P->dry)
@@ -671,14 +736,15 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
     const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
     if (l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
     if (!P->dry)
-        ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, s));
+        ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
+                               attn_bits(P, l, 1, b0), s));
     if (f8) {
         if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
         ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, &dr_cross));
     } else {
         ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E));
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, nullptr, &dr_cross));
     }
     // MLP (src/model.py:331-334, 262-267)
     if (!P->dry)
@@ -689,12 +755,12 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
                        ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
         if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
         ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, &dr_mlp));
     } else {
         ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF, ERGM_BF16,
                       ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
         ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E));
+                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, nullptr, &dr_mlp));
     }
     (void)L;
     return ERGM_OK;
@@ -719,6 +785,7 @@ int lmhead_split_cols(int T, int Vp) {
 
 int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s) {
     const ergm_model_dims& d = P->d;
+    P->drop_on = train != 0 && (P->p_attn > 0.f || P->p_resid > 0.f || P->p_embd > 0.f);
     const int T = P->T, E = d.n_embd, L = d.n_layer, B = d.batch, S = d.seq;
     const int L2E = P->L2E;
     const ergm_model_params& p = P->p;
@@ -749,10 +816,11 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         if (P->dry) return ERGM_OK;
         const int b0 = bsplit[c], nb = bsplit[c + 1] - b0;
         const size_t r0 = (size_t)b0 * S;
+        const ergm_dropout de = resid_drop(P, 0, b0);  // embedding dropout (src/model.py:506)
         return embed_fwd_ld(P->ids + r0, P->tt ? P->tt + r0 : nullptr, P->cap_ids + r0, p.wte, p.wpe,
                             vis_in ? vis_in + (size_t)b0 * ld_vis : nullptr, ld_vis,
                             aud_in ? aud_in + (size_t)b0 * E : nullptr, P->resid[0] + r0 * E, P->cap + r0 * P->XE,
-                            P->XE, nb, S, E, d.vocab, cs[c]);
+                            P->XE, nb, S, E, d.vocab, cs[c], drop_site_of(&de, E));
     };
     if (nchain == 2 && !P->dry) {
         if (hipEventRecord(P->ev_f2[0], s) != hipSuccess || hipStreamWaitEvent(P->fwd2, P->ev_f2[0], 0) != hipSuccess)
@@ -816,7 +884,7 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     }
     if (P->dry) return ERGM_OK;
     ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, emo_logits, P->emo_sum, nullptr, nullptr, P->emo_tmp,
-                               B, S, E, 7, P->B_global, nullptr, s));
+                               B, S, E, 7, P->n_valid ? P->n_valid + 1 : nullptr, nullptr, s));
     if (P->labels) {
         ERGM_TRY(ergm_xent_fwd_bwd(logits, d.vocab_pad, P->labels, P->n_valid, P->row_loss, train ? P->dlogits : nullptr,
                                    B, S, d.vocab, 1.0f, s));
@@ -827,7 +895,7 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     if (P->labels || P->emo_labels) {
         if (!P->labels) ERGM_TRY(hipMemsetAsync(P->row_loss, 0, (size_t)T * 4, s) == hipSuccess ? ERGM_OK : ERGM_EHIP);
         ERGM_TRY(ergm_loss_finalize(P->row_loss, T, P->labels ? P->n_valid : nullptr,
-                                    P->emo_labels ? P->emo_sum : nullptr, P->B_global, out_loss, s));
+                                    P->emo_labels ? P->emo_sum : nullptr, P->n_valid + 1, out_loss, s));
     }
     P->have_fwd = train != 0;
     return check_launch("model_forward");
@@ -869,7 +937,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     if (P->dry) return ERGM_OK;
     if (P->emo_labels) {
         ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w,
-                                   P->dy, P->emo_tmp + (size_t)B * 8 + 4, B, S, E, 7, P->B_global, gscale, s));
+                                   P->dy, P->emo_tmp + (size_t)B * 8 + 4, B, S, E, 7, P->n_valid + 1, gscale, s));
     } else {
         if (hipMemsetAsync(p.g_emo_w, 0, (size_t)7 * E * 4, s) != hipSuccess) return fail(ERGM_EHIP, "memset");
     }
@@ -908,8 +976,9 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     if (!P->dry) {
         const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
         __bf16* dkl = P->dkv_all + (size_t)l * 2 * E;
+        const ergm_dropout dp = attn_drop(P, l, 1, 0);
         ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, dxq, dkl, dkl + E, B, H, S, S, E,
-                               L2E, L2E, P->XE, E, E, L2E, L2E, 0, s));
+                               L2E, L2E, P->XE, E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, 0), s));
     }
     ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
     ERGM_TRY(gemm(P, s, T, E, E, dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
@@ -921,8 +990,10 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(gemm(P, s, T, E, E, dh1, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
                   ERGM_EPI_NONE));
     if (!P->dry) {
+        const ergm_dropout dp = attn_drop(P, l, 0, 0);
         ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, dqkv, dqkv + E,
-                               dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, s));
+                               dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, &dp,
+                               attn_bits(P, l, 0, 0), s));
     }
     ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
     ERGM_TRY(gemm(P, s, T, E, 3 * E, dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
@@ -941,6 +1012,10 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, L2E = P->L2E, L = d.n_layer;
+    if (!P->dry) {  // dh = gradient of the dropped embedding sum: through the embedding dropout (src/model.py:506)
+        const ergm_dropout de = resid_drop(P, 0, 0);
+        ERGM_TRY(dropout_apply_f32(drop_site_of(&de, E), P->dh, T, E, E, s));
+    }
     if (P->proj) {
         // feature projections: the projected vectors got dh0 at positions 0 / 1; dW = featᵀ·d over the
         // (padded) batch with the bias row fused (side stream); no gradient flows to the features

@@ -88,13 +88,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     }
 }
 
-// dx = rstd·(g − mean(g) − x̂·mean(g·x̂)), g = dy·γ;  dres += dx;  partial dγ = Σ dy·x̂, dβ = Σ dy
+// dx = rstd·(g − mean(g) − x̂·mean(g·x̂)), g = dy·γ;  dres += dx;  partial dγ = Σ dy·x̂, dβ = Σ dy.
+// dres_b = bf16(dres), or with `drop` the gradient reaching the residual branch that produced this
+// residual-stream tensor through its dropout: bf16(dres·keep/(1-p)) (src/model.py:245,266,506; the
+// keep bits recomputed, common.h drop_keep4).
 template <int NV>
 __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
-                                                     float* __restrict__ part_b, int rows, int E) {
+                                                     float* __restrict__ part_b, int rows, int E, DropSite drop) {
     __shared__ float red[2][LN_WAVES_BWD][NV * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 pg[NV], pb[NV], gm[NV];
@@ -163,7 +166,15 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                 *reinterpret_cast<float4*>(dres + (size_t)row * E + c) = v;
                 if (dres_b) {
                     bf16x4 ob;
-                    ob[0] = f2bf(v.x); ob[1] = f2bf(v.y); ob[2] = f2bf(v.z); ob[3] = f2bf(v.w);
+                    float4 u = v;
+                    if (drop.thresh) {
+                        const unsigned k = drop_keep4(drop, row, c);
+                        u.x = (k & 1u) ? u.x * drop.scale : 0.f;
+                        u.y = (k & 2u) ? u.y * drop.scale : 0.f;
+                        u.z = (k & 4u) ? u.z * drop.scale : 0.f;
+                        u.w = (k & 8u) ? u.w * drop.scale : 0.f;
+                    }
+                    ob[0] = f2bf(u.x); ob[1] = f2bf(u.y); ob[2] = f2bf(u.z); ob[3] = f2bf(u.w);
                     *reinterpret_cast<bf16x4*>(dres_b + (size_t)row * E + c) = ob;
                 }
             }
@@ -377,16 +388,17 @@ namespace ergm {
 int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
 
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
-                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s) {
+                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
+                       const DropSite& drop) {
     ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
-        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E); break;
+        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
+        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
+        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
+        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
     }
     return check_launch("layernorm_bwd");
 }
@@ -411,14 +423,16 @@ int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, i
 
 extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
                                   const float* gamma, float* dres, void* dres_bf16, float* dgamma, float* dbeta,
-                                  void* ws, size_t ws_bytes, int rows, int E, void* stream) {
+                                  void* ws, size_t ws_bytes, int rows, int E, const ergm_dropout* dropout,
+                                  void* stream) {
     ERGM_CHECK_ARG(dgamma && dbeta, "layernorm_bwd: null argument");
+    ERGM_TRY(check_dropout(dropout));
     ERGM_CHECK_ARG(ws && ws_bytes >= ergm_layernorm_bwd_workspace_size(rows, E), "layernorm_bwd: workspace too small");
     const int nb = ln_bwd_nparts(rows);
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
     hipStream_t s = as_stream(stream);
-    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s));
+    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E)));
     return layernorm_param_reduce(pg, pb, rows, E, dgamma, dbeta, s);
 }
 

@@ -113,28 +113,46 @@ __global__ __launch_bounds__(XE_THREADS) void xent_kernel(const __bf16* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void count_valid_kernel(const int64_t* __restrict__ labels, int B, int S,
+// counts[0] = LM rows the CE scores (label at s >= 1 scores logits row s-1; valid iff 0 <= y < V, the
+// predicate xent_kernel uses), counts[1] = valid emotion labels (0 <= y < C; -100 = ignore_index).
+__global__ __launch_bounds__(256) void count_valid_kernel(const int64_t* __restrict__ labels,
+                                                          const int64_t* __restrict__ emo, int B, int S, int V, int C,
                                                           int* __restrict__ out) {
-    __shared__ int red[4];
-    int c = 0;
-    for (int i = threadIdx.x; i < B * S; i += 256) {
-        int s = i % S;
-        if (s >= 1 && labels[i] != -100) ++c;  // label at s scores logits row s-1
-    }
+    __shared__ int red[2][4];
+    int c = 0, ce = 0;
+    if (labels)
+        for (int i = threadIdx.x; i < B * S; i += 256) {
+            const int64_t y = labels[i];
+            if (i % S >= 1 && y >= 0 && y < V) ++c;
+        }
+    if (emo)
+        for (int i = threadIdx.x; i < B; i += 256) ce += emo[i] >= 0 && emo[i] < C;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, 64);
+        ce += __shfl_xor(ce, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = c;
+        red[1][threadIdx.x >> 6] = ce;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) {
+        out[0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        out[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    }
 }
 
 // Emotion head, one workgroup per sample b: logits[b][c] = h[b,S-1,:]·W[c,:]; with labels the row
 // loss and dlogits go to `scratch` ([B][C] dlogits then [B] row losses) and, with dh,
-// dh[b,S-1,:] += dlogits[b]·W.
+// dh[b,S-1,:] += dlogits[b]·W.  CrossEntropyLoss semantics (src/model.py:710-711): labels outside
+// [0, C) (-100 = ignore_index) contribute neither loss nor gradient; the mean is over the n_valid
+// (global) valid labels.
 __global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restrict__ h, const float* __restrict__ W,
                                                           const int64_t* __restrict__ labels, float* __restrict__ logits,
                                                           float* __restrict__ scratch, float* __restrict__ dh, int B, int S,
-                                                          int E, int C, int B_global, const float* __restrict__ gscale) {
+                                                          int E, int C, const int* __restrict__ n_valid,
+                                                          const float* __restrict__ gscale) {
     __shared__ float lg[16], dl[16];
     const int b = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -157,13 +175,15 @@ __global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restri
         for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[c]);
         float se = 0.f;
         for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
-        const int y = (int)labels[b];
+        const int64_t y = labels[b];
+        const bool valid = y >= 0 && y < C;
+        const float inv_n = 1.0f / (float)max(1, *n_valid);
         for (int c = 0; c < C; ++c) {
-            float d = (expf(lg[c] - mx) / se - (c == y ? 1.f : 0.f)) * gs / (float)B_global;
+            const float d = valid ? (expf(lg[c] - mx) / se - (c == y ? 1.f : 0.f)) * gs * inv_n : 0.f;
             dl[c] = d;
             scratch[(size_t)b * C + c] = d;
         }
-        scratch[(size_t)B * C + b] = (mx + logf(se)) - lg[y];
+        scratch[(size_t)B * C + b] = valid ? (mx + logf(se)) - lg[y] : 0.f;
     }
     __syncthreads();
     if (!dh) return;
@@ -202,8 +222,8 @@ __global__ __launch_bounds__(256) void emotion_dw_kernel(const __bf16* __restric
 
 __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restrict__ row_loss, int T,
                                                             const int* __restrict__ n_valid,
-                                                            const float* __restrict__ emo_sum, int B_global,
-                                                            float* __restrict__ out) {
+                                                            const float* __restrict__ emo_sum,
+                                                            const int* __restrict__ n_emo, float* __restrict__ out) {
     __shared__ float red[4];
     float s = 0.f;
     for (int i = threadIdx.x; i < T; i += 256) s += row_loss[i];
@@ -215,7 +235,7 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restr
         // mean over the valid labels; none valid gives 0/0 = NaN, as torch's CrossEntropyLoss does for the
         // reference (src/model.py:704-709; the dlogits of ignored rows stay 0, as its gradient does)
         lm = n_valid ? lm / (float)(*n_valid) : 0.f;
-        float emo = emo_sum ? *emo_sum / (float)B_global : 0.f;
+        float emo = emo_sum ? *emo_sum / (float)(*n_emo) : 0.f;  // likewise 0/0 = NaN with no valid label
         out[0] = lm;
         out[1] = emo;
         out[2] = lm + emo;
@@ -226,9 +246,11 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restr
 
 using namespace ergm;
 
-extern "C" int ergm_count_valid(const int64_t* labels, int B, int S, int* n_valid, void* stream) {
-    ERGM_CHECK_ARG(labels && n_valid && B > 0 && S > 0, "count_valid: bad argument");
-    hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, as_stream(stream), labels, B, S, n_valid);
+extern "C" int ergm_count_valid(const int64_t* labels, const int64_t* emotion_labels, int B, int S, int V, int C,
+                                int* counts, void* stream) {
+    ERGM_CHECK_ARG(counts && B > 0 && S > 0 && V > 0 && C > 0, "count_valid: bad argument");
+    hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, as_stream(stream), labels, emotion_labels, B, S, V, C,
+                       counts);
     return check_launch("count_valid");
 }
 
@@ -252,18 +274,17 @@ extern "C" int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* lab
 }
 
 extern "C" int ergm_emotion_head(const void* h, const float* W, const int64_t* labels, float* logits, float* loss_sum,
-                                 float* dW, float* dh, float* scratch, int B, int S, int E, int C, int B_global,
-                                 const float* grad_scale_dev, void* stream) {
+                                 float* dW, float* dh, float* scratch, int B, int S, int E, int C,
+                                 const int* n_valid_global, const float* grad_scale_dev, void* stream) {
     ERGM_CHECK_ARG(h && W && logits, "emotion_head: null argument");
     ERGM_CHECK_ARG(B > 0 && C > 0 && C <= 16 && E > 0 && S > 0, "emotion_head: bad shape");
-    ERGM_CHECK_ARG(!labels || (loss_sum && scratch), "emotion_head: labels need loss_sum and scratch");
+    ERGM_CHECK_ARG(!labels || (loss_sum && scratch && n_valid_global), "emotion_head: labels need loss_sum, scratch and n_valid");
     ERGM_CHECK_ARG((dW == nullptr) == (dh == nullptr), "emotion_head: dW and dh go together");
     ERGM_CHECK_ARG(!dW || labels, "emotion_head: gradients need labels");
     hipStream_t s = as_stream(stream);
     const __bf16* hb = reinterpret_cast<const __bf16*>(h);
-    const int bg = B_global > 0 ? B_global : B;
-    hipLaunchKernelGGL(emotion_row_kernel, dim3(B), dim3(256), 0, s, hb, W, labels, logits, scratch, dh, B, S, E, C, bg,
-                       grad_scale_dev);
+    hipLaunchKernelGGL(emotion_row_kernel, dim3(B), dim3(256), 0, s, hb, W, labels, logits, scratch, dh, B, S, E, C,
+                       n_valid_global, grad_scale_dev);
     if (labels)
         hipLaunchKernelGGL(emotion_dw_kernel, dim3(dW ? cdiv(E, 256) : 1), dim3(256), 0, s, hb, scratch, loss_sum, dW,
                            B, S, E, C);
@@ -271,9 +292,10 @@ extern "C" int ergm_emotion_head(const void* h, const float* W, const int64_t* l
 }
 
 extern "C" int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
-                                  int B_global, float* out, void* stream) {
+                                  const int* n_valid_emo, float* out, void* stream) {
     ERGM_CHECK_ARG(row_loss && out && T > 0, "loss_finalize: bad argument");
+    ERGM_CHECK_ARG(!emo_loss_sum || n_valid_emo, "loss_finalize: the emotion loss needs its valid count");
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, as_stream(stream), row_loss, T, n_valid_global,
-                       emo_loss_sum, B_global > 0 ? B_global : 1, out);
+                       emo_loss_sum, n_valid_emo, out);
     return check_launch("loss_finalize");
 }

@@ -38,17 +38,23 @@ class DPSync:
         return dist.get_world_size(self.pg)
 
     @property
+    def rank(self) -> int:
+        if self.pg is None:
+            return 0
+        import torch.distributed as dist
+        return dist.get_rank(self.pg)
+
+    @property
     def active(self) -> bool:
         return self.world > 1
 
-    def reduce_count(self, n_valid: torch.Tensor) -> None:
-        """In place: local valid-label count -> global count (before the forward)."""
+    def reduce_count(self, counts: torch.Tensor) -> None:
+        """In place: local valid-label counts (LM, emotion) -> global counts (before the forward).
+        The loss means divide by these, so ranks with different batch sizes or ignored labels still
+        sum to the single-process gradient of the concatenated batch."""
         if self.active:
             import torch.distributed as dist
-            dist.all_reduce(n_valid, group=self.pg)
-
-    def global_batch(self, local_batch: int) -> int:
-        return local_batch * self.world
+            dist.all_reduce(counts, group=self.pg)
 
     def begin(self) -> None:
         self._works = []

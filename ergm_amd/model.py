@@ -15,11 +15,19 @@ Storage (see params.py): one fp32 ``nn.Parameter`` holding every weight, a bf16 
 MFMA GEMMs, one fp32 gradient buffer.  The whole forward is one native call and the backward three
 native stages per step (ergm_model_* in include/ergm_hip.h); there is no CPU fallback.
 
-Differences from the reference, by design: dropout is not supported (the parity path runs p=0);
-``logits`` come back as bf16 (the compute dtype) and are not differentiable (the reference trainer
-only back-propagates ``loss``); the KV-cache / ``past_key_values``, ``attention_mask``,
-``head_mask``, ``inputs_embeds`` and ``output_attentions`` paths are not part of the training hot
-path and raise ``NotImplementedError``.
+Dropout follows nn.Module semantics: in ``train()`` mode (the default, as the reference trainer runs,
+src/main.py:129) the attention-probability, residual-branch and embedding dropouts of the config
+(``attn_pdrop`` / ``resid_pdrop`` / ``embd_pdrop``, 0.1 like GPT2Config / the "gpt2" checkpoint) are
+applied with counter-based masks (include/ergm_hip.h ergm_dropout); ``eval()`` disables them.  The
+masks are drawn from ``torch``'s default generator at construction (``torch.manual_seed`` makes a run
+reproducible) and advance with every training forward.
+
+Differences from the reference, by design: ``logits`` come back as bf16 (the compute dtype) and are
+not differentiable (the reference trainer only back-propagates ``loss``); the KV-cache /
+``past_key_values``, ``attention_mask``, ``head_mask``, ``inputs_embeds`` and ``output_attentions``
+paths are not part of the training hot path and raise ``NotImplementedError``.  A second training
+forward of the same shape before the first one's backward raises in that backward (one set of saved
+activations per shape).
 """
 from __future__ import annotations
 
@@ -60,7 +68,9 @@ def _as_config(config) -> ERGMConfig:
     return ERGMConfig(vocab_size=g("vocab_size"), n_embd=g("n_embd"), n_layer=g("n_layer"), n_head=g("n_head"),
                       n_positions=g("n_positions", 1024), n_inner=g("n_inner"),
                       layer_norm_epsilon=g("layer_norm_epsilon", 1e-5),
-                      initializer_range=g("initializer_range", 0.02), feat_dim=g("feat_dim"))
+                      initializer_range=g("initializer_range", 0.02), feat_dim=g("feat_dim"),
+                      attn_pdrop=g("attn_pdrop", 0.1), resid_pdrop=g("resid_pdrop", 0.1),
+                      embd_pdrop=g("embd_pdrop", 0.1))
 
 
 class _FusedTrainStep(torch.autograd.Function):
@@ -70,8 +80,10 @@ class _FusedTrainStep(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, flat, model, runner, ids, tt, cap_ids, vis, aud, labels, emo_labels):
-        logits, emo, loss = runner.forward(ids, tt, cap_ids, vis, aud, labels, emo_labels, train=True)
+        logits, emo, loss = runner.forward(ids, tt, cap_ids, vis, aud, labels, emo_labels, train=True,
+                                           dropout=model._next_dropout())
         ctx.model, ctx.runner = model, runner
+        ctx.fwd_id = runner.fwd_count
         ctx.mark_non_differentiable(logits, emo)
         ctx.set_materialize_grads(False)
         return loss, logits, emo
@@ -82,6 +94,10 @@ class _FusedTrainStep(torch.autograd.Function):
             raise NotImplementedError("gradients through logits / emotion_logits are not supported; "
                                       "back-propagate the loss")
         model, runner = ctx.model, ctx.runner
+        if runner.fwd_count != ctx.fwd_id:
+            raise RuntimeError("another forward of the same (batch, seq) shape ran after this training forward and "
+                               "overwrote its saved activations: call backward() before the next forward of the "
+                               "shape (e.g. backward per micro-batch for gradient accumulation)")
         flat = model.flat
         gl = grad_loss
         if gl is not None:
@@ -130,6 +146,9 @@ class GPT2LMHeadModel(nn.Module):
         self._overlap_opt = None
         self._force_compact_lookup = False  # tests: the data-parallel wte path in one process
         self.process_group = process_group
+        # dropout mask stream: seed from torch's default generator, offset = training forwards so far
+        self._drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._drop_offset = 0
         self.init_weights()
 
     # ---- parameters / state_dict ---------------------------------------------------------
@@ -208,6 +227,15 @@ class GPT2LMHeadModel(nn.Module):
         return sum(self.layout.views[k].numel for k in state_dict_names(self.layout) if k != "lm_head.weight")
 
     # ---- forward ---------------------------------------------------------------------------
+    def _next_dropout(self):
+        """(attn_p, resid_p, embd_p, seed, offset) of the next training forward, None when every
+        probability is 0 or the module is in eval mode."""
+        c = self.config
+        if not self.training or not (c.attn_pdrop or c.resid_pdrop or c.embd_pdrop):
+            return None
+        self._drop_offset += 1
+        return (float(c.attn_pdrop), float(c.resid_pdrop), float(c.embd_pdrop), self._drop_seed, self._drop_offset)
+
     def _runner(self, B, S, vis_rows, has_feat) -> ModelRunner:
         key = (B, S, vis_rows, has_feat)
         r = self._runners.get(key)
@@ -237,6 +265,11 @@ class GPT2LMHeadModel(nn.Module):
         if caption_ids is None:
             # src/model.py:521 reads caption_embeds unconditionally: the reference cannot run without it
             raise ValueError("caption_ids is required (the reference forward reads caption embeddings in every block)")
+        if imgs is not None and visual_feat is None and torch.is_tensor(imgs) and imgs.dim() == 2:
+            # the reference adds imgs[i][0] to position 0 (src/model.py:497): for a 2-D [B, E] tensor that
+            # is the SCALAR imgs[i, 0], broadcast over the embedding (a [B, Tv, E] tensor gives row 0, the
+            # pooled vector; visual_feat= [B, E] is the build's vector form)
+            imgs = imgs[:, :1].expand(imgs.shape[0], self.layout.Fd).unsqueeze(1)
         vis = visual_feat if visual_feat is not None else imgs
         aud = audio_feat if audio_feat is not None else auds
         if (vis is None) != (aud is None):
@@ -252,6 +285,12 @@ class GPT2LMHeadModel(nn.Module):
             raise ValueError(f"caption_ids must have the text shape {(B, S)} (src/model.py:461), got {tuple(cap.shape)}")
         if tt is not None and tuple(tt.shape) != (B, S):
             raise ValueError("token_type_ids must match input_ids")
+        V = self.config.vocab_size
+        for name, t, hi in (("labels", labels, V), ("emotion_labels", emotion_labels, self.num_emotions)):
+            if t is not None and not t.is_cuda and t.numel():  # host labels: torch's range check, free here
+                bad = (t != -100) & ((t < 0) | (t >= hi))
+                if bool(bad.any()):
+                    raise IndexError(f"{name}: target {int(t[bad][0])} is out of bounds (classes: {hi})")
         lab = dv(labels, torch.int64)
         emo_lab = dv(emotion_labels, torch.int64)
         vis_rows = 0

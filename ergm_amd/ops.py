@@ -96,20 +96,58 @@ def quant_weight_fp8(W: torch.Tensor):
     return Wt, sc
 
 
-def attn_fwd(q, k, v, B, H, Sq, Sk, causal, o=None, lse=None):
-    """q/k/v: 2-D token-major views [B*S, ld] whose first column is head 0, dim 0."""
+def dropout_desc(p: float, seed: int, offset: int, site: int, row0: int = 0) -> L.Dropout:
+    """ergm_dropout for one site of one forward (include/ergm_hip.h)."""
+    return L.Dropout(seed=seed & (2 ** 64 - 1), offset=offset & 0xFFFFFFFF, site=site, p=p, row0=row0)
+
+
+def _dp(d: Optional[L.Dropout]):
+    return None if d is None else C.byref(d)
+
+
+def dropout_mask(d: L.Dropout, rows: int, cols: int, device) -> torch.Tensor:
+    """The keep mask of dropout site ``d`` over [rows, cols] as bool (ergm_dropout_mask's bits)."""
+    wpr = (cols + 31) // 32
+    bits = torch.empty(rows * wpr, dtype=torch.int32, device=device)
+    L.call("ergm_dropout_mask", C.byref(d), rows, cols, _ptr(bits), _stream(torch.device(device)))
+    return unpack_bits(bits.view(rows, wpr), cols, 32)
+
+
+def unpack_bits(words: torch.Tensor, cols: int, width: int) -> torch.Tensor:
+    """[rows, n] little-endian words of `width` (32 / 64) bits -> bool [rows, cols] (bit j of word w =
+    column width·w + j)."""
+    rows = words.shape[0]
+    b = words.contiguous().view(torch.uint8).view(rows, -1)            # little-endian bytes
+    shifts = torch.arange(8, device=b.device, dtype=torch.uint8)
+    bits = (b.unsqueeze(-1) >> shifts) & 1                               # [rows, bytes, 8]
+    return bits.view(rows, -1)[:, :cols].bool()
+
+
+def dropout_apply(x: torch.Tensor, d: L.Dropout) -> torch.Tensor:
+    """In place: x = keep ? x/(1-p) : 0 (f32 [rows, cols])."""
+    _need_gpu(x)
+    rows, cols = x.shape
+    L.call("ergm_dropout_apply", C.byref(d), _ptr(x), rows, cols, x.stride(0), _stream(x.device))
+    return x
+
+
+def attn_fwd(q, k, v, B, H, Sq, Sk, causal, o=None, lse=None, dropout: Optional[L.Dropout] = None):
+    """q/k/v: 2-D token-major views [B*S, ld] whose first column is head 0, dim 0.  With ``dropout``
+    also returns the keep bits the backward needs (u64 [B*H*Sq, ceil(Sk/64)])."""
     _need_gpu(q, k, v)
     dev = q.device
     if o is None:
         o = torch.empty(B * Sq, H * 64, dtype=torch.bfloat16, device=dev)
     if lse is None:
         lse = torch.empty(B, H, Sq, dtype=torch.float32, device=dev)
+    bits = torch.zeros(B * H * Sq, (Sk + 63) // 64, dtype=torch.int64, device=dev) if dropout is not None else None
     L.call("ergm_attn_fwd", _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, H, Sq, Sk, q.stride(0), k.stride(0),
-           v.stride(0), o.stride(0), int(bool(causal)), _stream(dev))
-    return o, lse
+           v.stride(0), o.stride(0), int(bool(causal)), _dp(dropout), _ptr(bits), _stream(dev))
+    return (o, lse) if dropout is None else (o, lse, bits)
 
 
-def attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal, dq=None, dk=None, dv=None):
+def attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal, dq=None, dk=None, dv=None,
+             dropout: Optional[L.Dropout] = None, keep_bits: Optional[torch.Tensor] = None):
     _need_gpu(q, k, v, o, dout, lse)
     dev = q.device
     dq = torch.empty(B * Sq, H * 64, dtype=torch.bfloat16, device=dev) if dq is None else dq
@@ -118,7 +156,7 @@ def attn_bwd(q, k, v, o, dout, lse, B, H, Sq, Sk, causal, dq=None, dk=None, dv=N
     delta = torch.empty(B, H, Sq, dtype=torch.float32, device=dev)
     L.call("ergm_attn_bwd", _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dq), _ptr(dk),
            _ptr(dv), B, H, Sq, Sk, q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0), dq.stride(0),
-           dk.stride(0), dv.stride(0), int(bool(causal)), _stream(dev))
+           dk.stride(0), dv.stride(0), int(bool(causal)), _dp(dropout), _ptr(keep_bits), _stream(dev))
     return dq, dk, dv
 
 
@@ -133,8 +171,9 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, dres):
-    """dres += LN_bwd(dy) in place; returns (dres, dres_bf16, dgamma, dbeta)."""
+def layernorm_bwd(dy, x, mean, rstd, gamma, dres, dropout: Optional[L.Dropout] = None):
+    """dres += LN_bwd(dy) in place; returns (dres, dres_bf16, dgamma, dbeta) (dres_bf16 through the
+    residual-branch ``dropout`` when given)."""
     _need_gpu(dy, x, mean, rstd, gamma, dres)
     rows, E = x.shape
     lib = L.load()
@@ -144,7 +183,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dres):
     dg = torch.empty(E, dtype=torch.float32, device=x.device)
     dbe = torch.empty_like(dg)
     L.call("ergm_layernorm_bwd", _ptr(dy), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dres), _ptr(db), _ptr(dg),
-           _ptr(dbe), _ptr(ws), wsb, rows, E, _stream(x.device))
+           _ptr(dbe), _ptr(ws), wsb, rows, E, _dp(dropout), _stream(x.device))
     return dres, db, dg, dbe
 
 
@@ -160,7 +199,7 @@ def colsum(X, out=None, accumulate=False):
     return out
 
 
-def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None):
+def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None, dropout: Optional[L.Dropout] = None):
     _need_gpu(ids, cap_ids, wte, wpe)
     B, S = ids.shape
     V, E = wte.shape
@@ -171,7 +210,7 @@ def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None):
         vis = vis.contiguous()
         ld_vis = vis[0].numel() if vis.dim() == 3 else vis.shape[1]
     L.call("ergm_embed_fwd", _ptr(ids), _ptr(tt), _ptr(cap_ids), _ptr(wte), _ptr(wpe), _ptr(vis), ld_vis,
-           _ptr(aud), _ptr(h0), _ptr(cap), B, S, E, V, _stream(ids.device))
+           _ptr(aud), _ptr(h0), _ptr(cap), B, S, E, V, _dp(dropout), _stream(ids.device))
     return h0, cap
 
 
@@ -202,10 +241,11 @@ def embed_bwd(ids, tt, cap_ids, dh0, dcap, dwte, dwpe):
            _ptr(ws), wsb, B, S, E, V, _stream(ids.device))
 
 
-def count_valid(labels):
+def count_valid(labels, emotion_labels=None, V: int = 2 ** 31 - 1, C_emo: int = 7):
+    """int32 [2] on the device: valid LM labels (s >= 1, 0 <= y < V) and valid emotion labels."""
     B, S = labels.shape
-    out = torch.empty(1, dtype=torch.int32, device=labels.device)
-    L.call("ergm_count_valid", _ptr(labels), B, S, _ptr(out), _stream(labels.device))
+    out = torch.empty(2, dtype=torch.int32, device=labels.device)
+    L.call("ergm_count_valid", _ptr(labels), _ptr(emotion_labels), B, S, V, C_emo, _ptr(out), _stream(labels.device))
     return out
 
 
@@ -219,15 +259,18 @@ def xent(logits, labels, n_valid, V, with_grad=True):
     return rl, dl
 
 
-def emotion_head(h, W, labels, B, S, B_global=None, dh=None, grad_scale=None):
+def emotion_head(h, W, labels, B, S, n_valid=None, dh=None, grad_scale=None):
+    """``n_valid``: device int32 count of valid labels (default: counted from ``labels``)."""
     E = h.shape[-1]
     Cn = W.shape[0]
     logits = torch.empty(B, Cn, dtype=torch.float32, device=h.device)
     loss_sum = torch.empty(1, dtype=torch.float32, device=h.device)
     dW = torch.empty_like(W) if dh is not None else None
     scratch = torch.empty(B * (Cn + 1), dtype=torch.float32, device=h.device)
+    if labels is not None and n_valid is None:
+        n_valid = ((labels >= 0) & (labels < Cn)).sum().to(torch.int32).reshape(1)
     L.call("ergm_emotion_head", _ptr(h), _ptr(W), _ptr(labels), _ptr(logits), _ptr(loss_sum), _ptr(dW), _ptr(dh),
-           _ptr(scratch), B, S, E, Cn, B_global or B, _ptr(grad_scale), _stream(h.device))
+           _ptr(scratch), B, S, E, Cn, _ptr(n_valid), _ptr(grad_scale), _stream(h.device))
     return logits, loss_sum, dW
 
 

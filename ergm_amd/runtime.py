@@ -86,8 +86,11 @@ class ModelRunner:
         L.check(self.lib.ergm_model_set_side_joins(self.plan, int(self.per_stage_join)), "ergm_model_set_side_joins")
         self.grad = grad
         self.dp = DPSync(process_group, dp_buckets(layout))
-        self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)  # [LM, emotion] valid-label counts
         self._inputs = None
+        # every forward overwrites the activations saved for backward: the autograd bridge checks that
+        # the forward it differentiates is still the runner's last one
+        self.fwd_count = 0
         # rows of the tied wte the batch's lookups touch (written by every training forward)
         self.row_flags = torch.zeros(layout.vocab_pad, dtype=torch.uint8, device=self.dev)
         L.check(self.lib.ergm_model_set_row_flags(self.plan, _p(self.row_flags), layout.vocab_pad),
@@ -150,18 +153,27 @@ class ModelRunner:
         return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
     # ---- forward ------------------------------------------------------------------------
-    def forward(self, ids, tt, cap_ids, vis, aud, labels, emo_labels, train: bool):
-        """Returns (logits [B*S, Vp] bf16, emotion_logits [B, 7] f32, loss3 [3] f32 or None)."""
+    def forward(self, ids, tt, cap_ids, vis, aud, labels, emo_labels, train: bool, dropout=None):
+        """Returns (logits [B*S, Vp] bf16, emotion_logits [B, 7] f32, loss3 [3] f32 or None).
+        ``dropout`` = (attn_p, resid_p, embd_p, seed, offset) for a training forward (None: no dropout)."""
         dev, B, S = self.dev, self.B, self.S
         s = self._stream()
-        if labels is not None:
-            L.check(self.lib.ergm_count_valid(_p(labels), B, S, _p(self.n_valid), s), "ergm_count_valid")
-            self.dp.reduce_count(self.n_valid[:1])
-        B_global = self.dp.global_batch(B)
+        have_labels = labels is not None or emo_labels is not None
+        if have_labels:
+            from .config import NUM_EMOTIONS
+            L.check(self.lib.ergm_count_valid(_p(labels), _p(emo_labels), B, S, self.layout.vocab, NUM_EMOTIONS,
+                                              _p(self.n_valid), s), "ergm_count_valid")
+            self.dp.reduce_count(self.n_valid[:2])
         self._inputs = (ids, tt, cap_ids, vis, aud, labels, emo_labels)  # keep alive through backward
         L.check(self.lib.ergm_model_set_inputs(self.plan, _p(ids), _p(tt), _p(cap_ids), _p(vis), _p(aud), _p(labels),
-                                               _p(emo_labels), _p(self.n_valid) if labels is not None else None,
-                                               B_global), "ergm_model_set_inputs")
+                                               _p(emo_labels), _p(self.n_valid) if have_labels else None),
+                "ergm_model_set_inputs")
+        pa, pr, pe, seed, offset = dropout if (dropout is not None and train) else (0.0, 0.0, 0.0, 0, 0)
+        # rows counted from this rank's first global sample: DP ranks draw the masks one process would
+        # draw for the concatenated batch (equal local batches)
+        L.check(self.lib.ergm_model_set_dropout(self.plan, pa, pr, pe, seed & (2 ** 64 - 1), offset & 0xFFFFFFFF,
+                                                self.dp.rank * B), "ergm_model_set_dropout")
+        self.fwd_count += 1
         logits = torch.empty(B * S, self.layout.vocab_pad, dtype=torch.bfloat16, device=dev)
         emo = torch.empty(B, 7, dtype=torch.float32, device=dev)
         loss = torch.empty(3, dtype=torch.float32, device=dev) if (labels is not None or emo_labels is not None) else None

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 2
+#define ERGM_ABI_VERSION 3
 
 typedef enum {
     ERGM_OK = 0,
@@ -44,6 +44,38 @@ typedef enum {
     ERGM_EUNSUPPORTED = -2,  /* valid request this build does not implement */
     ERGM_EHIP = -3,          /* HIP launch / runtime failure (hipError_t in the message) */
 } ergm_status;
+
+/* Dropout (nn.Dropout of the reference model in training mode: attention probabilities
+ * src/model.py:142, attention / cross-attention resid_dropout :245, MLP dropout :266, embedding
+ * dropout :506; p = GPT2Config attn_pdrop / resid_pdrop / embd_pdrop, 0.1 for the "gpt2" checkpoint
+ * src/main.py:62).  The keep decision of element (row, col) of a dropout site is a pure function of
+ * (seed, offset, site, row0 + row, col): Philox4x32-10 with key = seed and counter =
+ * {g mod 2^32, g >> 32, site, offset}, g = (row0 + row)·ceil(cols/4) + col/4; the element takes word
+ * (col mod 4) and is dropped iff that word < round(p·2^32); kept elements are scaled by 1/(1-p).
+ * Backward passes recompute the elementwise sites' bits; the attention forward stores its keep bits
+ * (1 bit per probability, ergm_attn_fwd) for the backward.  For the elementwise sites rows are
+ * tokens (b·S + s) and cols = n_embd; for attention probabilities rows are (b·H + h)·Sq + q and
+ * cols = Sk.  p = 0 or a NULL descriptor: no dropout.                                               */
+typedef struct {
+    uint64_t seed;
+    uint32_t offset;   /* forward number: every training forward draws fresh masks */
+    uint32_t site;     /* which nn.Dropout: ergm_drop_site */
+    float p;           /* drop probability, [0, 1) */
+    int64_t row0;      /* global row of the caller's row 0 (data-parallel ranks, batch slices) */
+} ergm_dropout;
+
+/* Site numbering of the executor (L blocks): 0 = embedding dropout; 3l+1 / 3l+2 / 3l+3 = the
+ * attention / cross-attention / MLP residual-branch dropout of block l (the residual-stream tensor
+ * they produce); 3L+1+2l / 3L+2+2l = attention / cross-attention probabilities of block l. */
+#define ERGM_DROP_SITE_EMBD 0u
+#define ERGM_DROP_SITE_RESID(l, k) (3u * (uint32_t)(l) + 1u + (uint32_t)(k)) /* k: 0 attn, 1 cross, 2 mlp */
+#define ERGM_DROP_SITE_ATTN(L, l, cross) (3u * (uint32_t)(L) + 1u + 2u * (uint32_t)(l) + ((cross) ? 1u : 0u))
+
+/* The keep mask itself: bits[r][w], ceil(cols/32) words per row, bit j of word w = element
+ * (r, 32w + j) kept (pad bits 0).  Tests replay these masks through the CPU oracle.               */
+int ergm_dropout_mask(const ergm_dropout* d, int rows, int cols, uint32_t* bits, void* stream);
+/* x[r][c] = keep ? x·1/(1-p) : 0, in place (f32, row stride ld; cols, ld multiples of 4). */
+int ergm_dropout_apply(const ergm_dropout* d, float* x, int rows, int cols, int ld, void* stream);
 
 typedef enum { ERGM_F32 = 0, ERGM_BF16 = 1 } ergm_dtype;
 
@@ -59,7 +91,8 @@ typedef enum { ERGM_NK = 0, ERGM_KN = 1 } ergm_b_layout;
  *   BIAS        C = v + bias[n]
  *   BIAS_GELU   aux_out[m][n] = bf16(v + bias[n]) (pre-activation, for backward);
  *               C = gelu_new(v + bias[n])
- *   BIAS_RESID  C(f32) = aux[m][n](f32) + (v + bias[n])          (residual add; aux may == C)
+ *   BIAS_RESID  C(f32) = aux[m][n](f32) + drop(v + bias[n])      (residual add; aux may == C;
+ *               drop = the optional `dropout` site over [M][N], identity when NULL)
  *   GELU_BWD    C = v * gelu_new'(aux[m][n]) with aux = bf16 pre-activation
  *   ACCUM       C(f32) = C + v                                   (beta = 1 accumulation)          */
 typedef enum {
@@ -86,6 +119,7 @@ typedef struct {
     int ld_aux_out;
     int split_k;         /* 0 = choose automatically, 1 = none, >1 = forced split count */
     const float* alpha_dev;  /* optional device scalar multiplied into alpha (autograd grad_output) */
+    const ergm_dropout* dropout;  /* BIAS_RESID only: residual-branch dropout (rows m, cols n); NULL = none */
 } ergm_gemm_desc;
 
 /* Tuning hook (calling thread only): force pipelined-kernel configuration `cfg` (tile / wave grid /
@@ -127,14 +161,19 @@ int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K, int N, voi
 /* Fused attention over head_dim = 64, token-major tensors with head h at columns [64h, 64h+64):
  *   Q[b][s][h*64+d] = q + (b*Sq + s)*ldq + h*64 + d     (likewise K/V with Sk rows, O with ldo)
  * out: O (bf16) and lse[b][h][s] = ln Σ_k exp(score) (f32; backward recomputes P from it).
- * `causal`: key j visible to query i iff j <= i (Sq == Sk required). scale = 1/sqrt(64).          */
+ * `causal`: key j visible to query i iff j <= i (Sq == Sk required). scale = 1/sqrt(64).
+ * dropout (optional, p > 0): O = (P∘keep/(1-p))·V with the keep bits of ergm_dropout_mask over rows
+ * (b·H + h)·Sq + q and cols Sk (the LSE stays that of the undropped softmax); the forward stores them
+ * in keep_bits: u64 [B·H·Sq][ceil(Sk/64)], bit key mod 64 of word key/64 (Sq, Sk <= 1024); the
+ * backward reads the same buffer.  NULL / p == 0: no dropout, keep_bits unused.                  */
 int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
-                  int Sq, int Sk, int ldq, int ldk, int ldv, int ldo, int causal, void* stream);
+                  int Sq, int Sk, int ldq, int ldk, int ldv, int ldo, int causal,
+                  const ergm_dropout* dropout, void* keep_bits, void* stream);
 /* delta workspace: B*H*Sq floats.  dq/dk/dv are bf16 with their own leading dims.              */
 int ergm_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                   const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
                   int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
-                  int causal, void* stream);
+                  int causal, const ergm_dropout* dropout, const void* keep_bits, void* stream);
 /* Path selection hook (tests / tuning): bit 0 of force_generic makes ergm_attn_bwd use the tiled
  * kernels even where the one-workgroup-per-(b,h) kernel applies (Sq, Sk <= 128; the forward is tiled at
  * every length); bits 4-7 select the
@@ -145,26 +184,29 @@ int ergm_attn_tune(int force_generic);
 /* LayerNorm over rows of E (biased variance, eps): y(bf16) = (x-μ)·rstd·γ + β; x f32.        */
 int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
                        float* rstd, int rows, int E, float eps, void* stream);
-/* dres(f32, in/out) += LN_bwd(dy); dres_bf16 (optional) = bf16(dres); dγ/dβ (f32 [E], written).
+/* dres(f32, in/out) += LN_bwd(dy); dres_bf16 (optional) = bf16(dres), or bf16(dres·keep/(1-p))
+ * with `dropout` (rows x E): the gradient of the residual branch whose dropped output was added into
+ * this residual-stream tensor; dγ/dβ (f32 [E], written).
  * workspace: ergm_layernorm_bwd_workspace_size(rows, E) bytes.                                  */
 size_t ergm_layernorm_bwd_workspace_size(int rows, int E);
 int ergm_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
                        const float* gamma, float* dres, void* dres_bf16, float* dgamma, float* dbeta,
-                       void* workspace, size_t ws_bytes, int rows, int E, void* stream);
+                       void* workspace, size_t ws_bytes, int rows, int E, const ergm_dropout* dropout,
+                       void* stream);
 
 /* Column sums of a row-major matrix (bias gradients, wpe gradient): out[c] (=|+=) Σ_r X[r][c]. */
 size_t ergm_colsum_workspace_size(int rows, int cols);
 int ergm_colsum(const void* X, int x_dtype, int rows, int cols, int ldx, float* out, int accumulate,
                 void* workspace, size_t ws_bytes, void* stream);
 
-/* Embedding + fusion (src/model.py:459-463,495-504):
- *   h0[b,s] = ((wte[ids] + [s==0]·vis[b] + [s==1]·aud[b]) + wpe[s]) + wte[tt]      (f32)
- *   cap[b,s] = bf16(wte[cap_ids])
+/* Embedding + fusion (src/model.py:459-463,495-506):
+ *   h0[b,s] = drop(((wte[ids] + [s==0]·vis[b] + [s==1]·aud[b]) + wpe[s]) + wte[tt])      (f32)
+ *   cap[b,s] = bf16(wte[cap_ids])                       (caption embeddings are not dropped)
  * vis: [B][ld_vis] row b's first E values (imgs[i][0]); vis/aud may be NULL (text-only);
- * tt may be NULL.                                                                              */
+ * tt may be NULL; dropout (rows b·S + s, cols E) may be NULL.                                  */
 int ergm_embed_fwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte,
                    const float* wpe, const float* vis, int ld_vis, const float* aud, float* h0,
-                   void* cap, int B, int S, int E, int V, void* stream);
+                   void* cap, int B, int S, int E, int V, const ergm_dropout* dropout, void* stream);
 /* Feature pooling (data_process/feature_extraction.py:63,69: torch.mean(last_hidden_state, dim=1) of the
  * wav2vec2 / BLIP-vision encoder outputs): out[b][d] = mean_{t < len_b} x[b][t][d], x f32 or bf16 with
  * strides ld_t (frames) and ld_b (samples) in elements, lengths optional (NULL = all T frames; padded
@@ -184,21 +226,27 @@ int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
  * ignored, zeroed in dlogits).  Row t=(b,s) is valid iff s < S-1 and labels[b][s+1] != -100.
  * n_valid_global: device int (count of valid rows over all DP ranks).
  * row_loss[t] = lse - logit[target] (0 for invalid); dlogits = grad_scale·(softmax - onehot)/n_valid
- * (bf16, may be NULL for forward only).  ergm_count_valid writes the local count.             */
-int ergm_count_valid(const int64_t* labels, int B, int S, int* n_valid, void* stream);
+ * (bf16, may be NULL for forward only).  ergm_count_valid writes the local counts: counts[0] = LM
+ * labels at s >= 1 with 0 <= y < V, counts[1] = emotion labels with 0 <= y < C (either label tensor
+ * may be NULL: count 0).  Labels outside the range (-100 = torch's ignore_index) are ignored.       */
+int ergm_count_valid(const int64_t* labels, const int64_t* emotion_labels, int B, int S, int V, int C,
+                     int* counts, void* stream);
 int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* labels, const int* n_valid_global,
                       float* row_loss, void* dlogits, int B, int S, int V, float grad_scale,
                       void* stream);
 /* Emotion head on the last token: logits[b][c] = Σ_e h[b,S-1,e]·W[c][e] (h bf16, W f32 [C][E]);
- * with labels: loss_sum = Σ_b CE_b (the caller divides by B_global), scratch = B*(C+1) floats; with
- * dW/dh: dW[C][E] written and dh[b,S-1,:] += dlogits·W (f32 dh [B*S][E]), dlogits =
- * (softmax - onehot)·grad_scale/B_global.                                                       */
+ * with labels: loss_sum = Σ_b CE_b over valid labels (0 <= y < C; others, e.g. -100, are ignored),
+ * scratch = B*(C+1) floats, n_valid_global = device count of valid labels (all DP ranks); with dW/dh:
+ * dW[C][E] written and dh[b,S-1,:] += dlogits·W (f32 dh [B*S][E]), dlogits =
+ * (softmax - onehot)·grad_scale/n_valid (0 for ignored labels).                                  */
 int ergm_emotion_head(const void* h, const float* W, const int64_t* labels, float* logits,
                       float* loss_sum, float* dW, float* dh, float* scratch, int B, int S, int E, int C,
-                      int B_global, const float* grad_scale_dev, void* stream);
-/* out[0] = Σ row_loss / n_valid_global (0 if n_valid_global is NULL), out[1] = emo_loss_sum / B_global, out[2] = out[0]+out[1]. */
+                      const int* n_valid_global, const float* grad_scale_dev, void* stream);
+/* out[0] = Σ row_loss / n_valid_global (0 if n_valid_global is NULL), out[1] = emo_loss_sum /
+ * n_valid_emo (0 if emo_loss_sum is NULL), out[2] = out[0]+out[1]; a zero count gives 0/0 = NaN,
+ * as torch's mean CrossEntropyLoss does.                                                         */
 int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
-                       const float* emo_loss_sum, int B_global, float* out, void* stream);
+                       const float* emo_loss_sum, const int* n_valid_emo, float* out, void* stream);
 
 /* torch.optim.AdamW step over flat fp32 arrays; also refreshes the bf16 shadow copy.
  * Arithmetic in torch's order: p*=(1-lr·wd); m=lerp(m,g,1-β1); v=β2·v+(1-β2)g²;
@@ -282,8 +330,8 @@ int ergm_model_create(const ergm_model_dims* dims, const ergm_model_params* para
                       size_t ws_bytes, ergm_model_plan** out_plan);
 int ergm_model_destroy(ergm_model_plan* plan);
 /* Inputs for the next forward (device pointers, int64 [B][S]; features f32 or NULL; labels may be
- * NULL for inference).  n_valid_global: device int the caller filled (ergm_count_valid +
- * optional all-reduce); B_global: global batch for the emotion-loss mean.                       */
+ * NULL for inference).  counts_global: device int[2] the caller filled (ergm_count_valid + optional
+ * all-reduce over DP ranks): the LM and the emotion loss means divide by these global counts.     */
 /* Optional: a caller-owned byte per padded vocabulary row (n >= vocab_pad).  When set, every training
  * forward writes 1 for the rows its token / token-type / caption lookups touch and 0 elsewhere
  * (stream-ordered, final once the forward returns on its stream).  The lookup gradients of the
@@ -304,7 +352,7 @@ int ergm_rows_compact(const void* row_flag, const int* pos, int n, int row_len, 
 int ergm_model_set_inputs(ergm_model_plan* plan, const int64_t* ids, const int64_t* tt,
                           const int64_t* cap_ids, const float* vis, const float* aud,
                           const int64_t* labels, const int64_t* emotion_labels,
-                          const int* n_valid_global, int B_global);
+                          const int* counts_global);
 /* Forward. Outputs (device): logits bf16 [B*S][vocab_pad], emotion logits f32 [B][7],
  * loss parts f32 (ergm_loss_finalize layout: [lm, emotion, total], local contributions over the
  * global normalisers); with `train`, dlogits are prepared for the backward.                      */
@@ -320,6 +368,15 @@ int ergm_model_forward(ergm_model_plan* plan, void* logits, float* emo_logits, f
 int ergm_model_backward_head(ergm_model_plan* plan, const float* grad_scale_dev, void* stream);
 int ergm_model_backward_layer(ergm_model_plan* plan, int layer, void* stream);
 int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
+/* Dropout of the next training forwards (ergm_model_forward with train = 1) and their backward:
+ * attn_p = attention probabilities (src/model.py:142), resid_p = the attention / cross-attention /
+ * MLP residual branches (:245, :266), embd_p = the embeddings (:506); all 0 = the deterministic path
+ * (default).  Masks are ergm_dropout_mask's with this seed and offset (the caller advances offset
+ * every training forward), site numbers ERGM_DROP_SITE_*, rows counted from global sample
+ * batch_base (data parallelism: rank·batch, so DP ranks draw exactly the masks one process would
+ * draw for the concatenated batch).  Inference forwards (train = 0) never drop.                  */
+int ergm_model_set_dropout(ergm_model_plan* plan, float attn_p, float resid_p, float embd_p, uint64_t seed,
+                           uint32_t offset, int batch_base);
 /* Side-stream joins.  per_stage = 1 (default): the ordering guarantee above.  per_stage = 0: the
  * caller's stream does not wait for block l+1's weight gradients at the end of stage l (so the
  * data-gradient chain never idles behind the weight-gradient GEMMs); only backward_embed joins, after

@@ -151,8 +151,18 @@ def _merge_heads(t: torch.Tensor) -> torch.Tensor:  # src/model.py:195-198
     return t.permute(0, 2, 1, 3).contiguous().view(B, S, H * d)
 
 
-def _attn(q, k, v, causal: bool, mask_add: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``GPT2Attention._attn`` src/model.py:119-148 (scale_attn_weights=True, no layer-idx scaling)."""
+def _drop(x: torch.Tensor, keep: Optional[torch.Tensor], p: float) -> torch.Tensor:
+    """``nn.Dropout`` in training mode with a given keep mask: x · keep · 1/(1-p) (torch scales the
+    bernoulli noise by 1/(1-p) in the tensor's dtype).  keep None: identity (eval / p = 0)."""
+    if keep is None or p == 0.0:
+        return x
+    return x * (keep.to(x.dtype) * torch.full([], 1.0 / (1.0 - p), dtype=torch.float32).to(x.dtype))
+
+
+def _attn(q, k, v, causal: bool, mask_add: Optional[torch.Tensor] = None, keep: Optional[torch.Tensor] = None,
+          p: float = 0.0) -> torch.Tensor:
+    """``GPT2Attention._attn`` src/model.py:119-148 (scale_attn_weights=True, no layer-idx scaling;
+    ``attn_dropout`` on the probabilities :142 with the given keep mask [B, H, Sq, Sk])."""
     w = torch.matmul(q, k.transpose(-1, -2))
     w = w / torch.full([], v.size(-1) ** 0.5, dtype=w.dtype)
     if causal:
@@ -162,6 +172,7 @@ def _attn(q, k, v, causal: bool, mask_add: Optional[torch.Tensor] = None) -> tor
     if mask_add is not None:
         w = w + mask_add
     w = F.softmax(w, dim=-1)
+    w = _drop(w, keep, p)
     return torch.matmul(w, v)
 
 
@@ -171,18 +182,37 @@ def _layer_norm(x, P, name, eps):
 
 def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type_ids=None,
             caption_ids=None, visual_feat=None, audio_feat=None, labels=None,
-            emotion_labels=None) -> Dict[str, torch.Tensor]:
+            emotion_labels=None, imgs=None, dropout=None) -> Dict[str, torch.Tensor]:
     """Fused model forward (``GPT2LMHeadModel.forward`` src/model.py:654-737).
 
-    ``visual_feat`` is ``imgs``: [B, E] (the vector itself) or [B, Tv, E] (row 0 used, ``imgs[i][0]``
-    src/model.py:497); ``audio_feat`` is ``auds`` [B, E] (:498).  ``caption_ids`` [B, S] is
-    mandatory, as in the only runnable reference call.
+    ``visual_feat`` is the pooled visual vector per sample: [B, E], or [B, Tv, E] (row 0 used,
+    ``imgs[i][0]`` src/model.py:497).  ``imgs`` is the reference's own argument: ``imgs[i][0]`` is added
+    to position 0, so a 2-D [B, E] ``imgs`` contributes the SCALAR imgs[i, 0] (broadcast) and a 3-D one
+    its row 0.  ``audio_feat`` is ``auds`` [B, E] (:498).  ``caption_ids`` [B, S] is mandatory, as in
+    the only runnable reference call.
+
+    ``dropout`` = (attn_p, resid_p, embd_p, keep) replays training-mode dropout (src/model.py:142,245,
+    266,506) with given keep masks: keep[site] bool, site numbers of include/ergm_hip.h (0 embeddings
+    [B·S, E]; 3l+1..3l+3 the residual branches of block l [B·S, E]; 3L+1+2l / 3L+2+2l the attention /
+    cross-attention probabilities of block l [B·H·S, Sk]).
     """
     if caption_ids is None:
         raise ValueError("caption_ids is required (src/model.py:521 reads caption_embeds unconditionally)")
     E, H, L, eps = cfg.n_embd, cfg.n_head, cfg.n_layer, cfg.layer_norm_epsilon
     wte, wpe = P["transformer.wte.weight"], P["transformer.wpe.weight"]
     B, S = input_ids.shape
+    pa = pr = pe = 0.0
+    keep = {}
+    if dropout is not None:
+        pa, pr, pe, keep = dropout
+
+    def km(site, shape):  # keep mask of a site in the tensor's shape
+        k = keep.get(site)
+        return None if k is None else k.reshape(shape)
+    if imgs is not None:
+        if visual_feat is not None:
+            raise ValueError("give imgs (reference semantics) or visual_feat, not both")
+        visual_feat = imgs[:, :1].expand(B, imgs.shape[1]) if imgs.dim() == 2 else imgs
     inputs_embeds = F.embedding(input_ids, wte)                               # :459
     # :460-463 views captions as [-1, S] (caption length == S); [B, -1] is the same for Sc == S and
     # lets the KV-cache generation test score a response against fixed prompt captions (Sc != S)
@@ -202,13 +232,17 @@ def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type
     h = inputs_embeds + pos                                                   # :501
     if token_type_ids is not None:
         h = h + F.embedding(token_type_ids, wte)                              # :502-504
+    h = _drop(h, km(0, (B, S, E)), pe)                                        # :506
+    Sc = caption_embeds.shape[1]
     for i in range(L):                                                        # :520-576
         p = f"transformer.h.{i}."
         r = h                                                                 # self-attn :297-309
         x = _layer_norm(h, P, p + "ln_1", eps)
         q, k, v = _conv1d(x, P[p + "attn.c_attn.weight"], P[p + "attn.c_attn.bias"]).split(E, dim=2)
-        a = _attn(_split_heads(q, H), _split_heads(k, H), _split_heads(v, H), causal=True)
+        a = _attn(_split_heads(q, H), _split_heads(k, H), _split_heads(v, H), causal=True,
+                  keep=km(3 * L + 1 + 2 * i, (B, H, S, S)), p=pa)
         a = _conv1d(_merge_heads(a), P[p + "attn.c_proj.weight"], P[p + "attn.c_proj.bias"])
+        a = _drop(a, km(3 * i + 1, (B, S, E)), pr)                            # resid_dropout :245
         h = a + r
         r = h                                                                 # cross-attn :311-329
         x = _layer_norm(h, P, p + "ln_cross_attn", eps)
@@ -216,15 +250,17 @@ def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type
         k, v = _conv1d(caption_embeds, P[p + "crossattention.c_attn.weight"],
                        P[p + "crossattention.c_attn.bias"]).split(E, dim=2)
         a = _attn(_split_heads(q, H), _split_heads(k, H), _split_heads(v, H), causal=False,
-                  mask_add=enc_mask)
+                  mask_add=enc_mask, keep=km(3 * L + 2 + 2 * i, (B, H, S, Sc)), p=pa)
         a = _conv1d(_merge_heads(a), P[p + "crossattention.c_proj.weight"],
                     P[p + "crossattention.c_proj.bias"])
+        a = _drop(a, km(3 * i + 2, (B, S, E)), pr)                            # resid_dropout :245
         h = r + a
         r = h                                                                 # MLP :331-334
         x = _layer_norm(h, P, p + "ln_2", eps)
         x = _conv1d(x, P[p + "mlp.c_fc.weight"], P[p + "mlp.c_fc.bias"])
         x = _gelu_new(x)
         x = _conv1d(x, P[p + "mlp.c_proj.weight"], P[p + "mlp.c_proj.bias"])
+        x = _drop(x, km(3 * i + 3, (B, S, E)), pr)                            # mlp dropout :266
         h = r + x
     h = _layer_norm(h, P, "transformer.ln_f", eps)                            # :578
     logits = F.linear(h, wte)                                                 # :698 (tied)
@@ -237,16 +273,16 @@ def forward(P: Dict[str, torch.Tensor], cfg: OracleConfig, input_ids, token_type
         out["loss_lm"] = F.cross_entropy(sl.view(-1, sl.size(-1)), lab.view(-1), ignore_index=-100)
         loss = out["loss_lm"]
     if emotion_labels is not None:
-        out["loss_emotion"] = F.cross_entropy(emo.view(-1, NUM_EMOTIONS), emotion_labels.view(-1))
+        out["loss_emotion"] = F.cross_entropy(emo.view(-1, NUM_EMOTIONS), emotion_labels.view(-1))  # ignore -100
         loss = out["loss_emotion"] if loss is None else loss + out["loss_emotion"]
     out["loss"] = loss
     return out
 
 
-def loss_and_grads(P: Dict[str, torch.Tensor], cfg: OracleConfig, batch: Dict[str, torch.Tensor]):
+def loss_and_grads(P: Dict[str, torch.Tensor], cfg: OracleConfig, batch: Dict[str, torch.Tensor], dropout=None):
     """Forward + ``loss.backward()`` (src/main.py:147-154); returns (outputs, grads by name)."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
-    out = forward(leaves, cfg, **batch)
+    out = forward(leaves, cfg, **batch, dropout=dropout)
     out["loss"].backward()
     grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v)
              for k, v in leaves.items()}

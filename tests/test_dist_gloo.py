@@ -24,6 +24,7 @@ def _batch():
     b = synthetic_batch(B, S, n_turns=3, feat_dim=CFG.n_embd, seed=9, vocab_hi=250, sp1=254, sp2=255, eos=249)
     b["labels"][1, :] = -100            # uneven valid-label counts across ranks
     b["labels"][1, -3:] = b["input_ids"][1, -3:]
+    b["emotion_labels"][0] = -100       # ignore_index: uneven valid emotion counts too
     return b
 
 
@@ -47,13 +48,14 @@ def _worker(rank, world, port, out_path):
     local = {k: v[lo:hi].clone() for k, v in full.items()}
     layout = build_layout(CFG.vocab_size, CFG.n_embd, CFG.n_layer, CFG.inner, CFG.n_positions)
     dp = DPSync(dist.group.WORLD, dp_buckets(layout))
-    n = (local["labels"][:, 1:] != -100).sum().reshape(1).to(torch.int32)
-    n_local = int(n.item())
+    n = torch.tensor([int((local["labels"][:, 1:] != -100).sum()), int((local["emotion_labels"] != -100).sum())],
+                     dtype=torch.int32)
+    n_local, e_local = n.tolist()
     dp.reduce_count(n)
-    n_global = int(n.item())
+    n_global, e_global = n.tolist()
     leaves = {k: v.clone().requires_grad_(True) for k, v in P.items()}
     out = O.forward(leaves, CFG, **local)
-    loss = out["loss_lm"] * (n_local / n_global) + out["loss_emotion"] * ((hi - lo) / dp.global_batch(hi - lo))
+    loss = out["loss_lm"] * (n_local / n_global) + out["loss_emotion"] * (e_local / e_global)
     loss.backward()
     grad = _flat_grads(layout, {k: v.grad for k, v in leaves.items()})
     dp.begin()

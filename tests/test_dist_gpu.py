@@ -17,8 +17,8 @@ B, S = 4, 32
 
 
 def _cfg():
-    from ergm_amd.config import ERGMConfig
-    return ERGMConfig(vocab_size=500, n_embd=128, n_layer=2, n_head=2, n_positions=64)
+    from ergm_amd.config import ERGMConfig, NO_DROPOUT
+    return ERGMConfig(vocab_size=500, n_embd=128, n_layer=2, n_head=2, n_positions=64, **NO_DROPOUT)
 
 
 def _batch():

@@ -13,7 +13,7 @@ The fp8 weights are re-quantised (from the bf16 shadow) at every forward.
 import pytest
 import torch
 
-from ergm_amd.config import ERGMConfig
+from ergm_amd.config import ERGMConfig, NO_DROPOUT
 from ergm_amd.data import synthetic_batch
 from ergm_amd.model import GPT2LMHeadModel
 from oracle import gpt2_oracle as O
@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 def _pair(V, E, Lyr, H, Fd, seed):
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, feat_dim=Fd)
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, feat_dim=Fd)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, feat_dim=Fd, **NO_DROPOUT)
     P0 = O.init_params(ocfg, seed=seed)
     return ocfg, cfg, P0
 

@@ -4,7 +4,7 @@ to the prompt's), within the bf16 logits gate; nucleus sampling is seeded-determ
 import pytest
 import torch
 
-from ergm_amd.config import ERGMConfig
+from ergm_amd.config import ERGMConfig, NO_DROPOUT
 from ergm_amd.generate import KVCacheGenerator
 from ergm_amd.model import GPT2LMHeadModel
 from oracle import gpt2_oracle as O
@@ -18,7 +18,7 @@ def _setup(gpu, feat_dim=None):
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P, feat_dim=feat_dim)
     P0 = O.init_params(ocfg, seed=11)
     model = GPT2LMHeadModel(ERGMConfig(vocab_size=V, n_embd=E, n_layer=LYR, n_head=H, n_positions=P,
-                                       feat_dim=feat_dim), device=gpu)
+                                       feat_dim=feat_dim, **NO_DROPOUT), device=gpu)
     model.load_state_dict(P0, strict=True)
     return ocfg, P0, model
 

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from ergm_amd.config import ERGMConfig
+from ergm_amd.config import ERGMConfig, NO_DROPOUT
 from ergm_amd.model import GPT2LMHeadModel
 from ergm_amd.optim import FusedAdamW
 from oracle import gpt2_oracle as O
@@ -33,7 +33,7 @@ def _load(name):
 def _setup(rec, gpu):
     V, E, Lyr, H, P = (int(x) for x in rec["config"])
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P)
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P, **NO_DROPOUT)
     P0 = O.init_params(ocfg, seed=int(rec["seed"]))
     model = GPT2LMHeadModel(cfg, device=gpu)
     model.load_state_dict(P0, strict=False)
@@ -223,7 +223,7 @@ def test_iemocap_shape_long_sequence_matches_oracle(gpu):
     from ergm_amd.data import synthetic_batch
     V, E, Lyr, H = 500, 128, 2, 2
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=512)
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=512)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=512, **NO_DROPOUT)
     P0 = O.init_params(ocfg, seed=7)
     model = GPT2LMHeadModel(cfg, device=gpu)
     model.load_state_dict(P0, strict=False)
@@ -243,7 +243,7 @@ def test_full_vocab_lm_head_at_c2_token_count(gpu):
     import bench
     from ergm_amd.data import synthetic_batch
     V, E, Lyr, H = 50260, 768, 1, 12
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, **NO_DROPOUT)
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
     P0 = O.init_params(ocfg, seed=11)
     model = GPT2LMHeadModel(cfg, device=gpu)
@@ -264,7 +264,7 @@ def test_full_vocab_lm_head_at_c2_token_count(gpu):
 
 
 def _small_model(gpu, S, seed, V=512, E=128, Lyr=2, H=2):
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, **NO_DROPOUT)
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
     P0 = O.init_params(ocfg, seed=seed)
     model = GPT2LMHeadModel(cfg, device=gpu)

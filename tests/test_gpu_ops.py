@@ -359,7 +359,7 @@ def test_cross_entropy(gpu, B, S, V, ldl):
     lb = _bf(logits)
     labels = torch.randint(0, V, (B, S), generator=g)
     labels[:, : S // 2] = -100
-    n = ops.count_valid(labels.to(gpu))
+    n = ops.count_valid(labels.to(gpu), V=V)[:1]
     rl, dl = ops.xent(lb.to(gpu), labels.to(gpu), n, V)
     x = lb[:, :V].float().reshape(B, S, V)[:, :-1].reshape(-1, V).requires_grad_(True)
     y = labels[:, 1:].reshape(-1)
@@ -372,21 +372,28 @@ def test_cross_entropy(gpu, B, S, V, ldl):
     assert _rel(got[:, :-1, :V].reshape(-1, V), x.grad) < 6e-3
 
 
-def test_emotion_head(gpu):
+@pytest.mark.parametrize("ignored", [0, 5])
+def test_emotion_head(gpu, ignored):
+    """CrossEntropyLoss semantics incl. ignore_index=-100 (those samples: no loss, no gradient; the mean
+    is over the valid labels, src/model.py:710-711)."""
     B, S, E, Cn = 16, 8, 768, 7
     h = torch.randn(B * S, E, device=gpu).bfloat16()
     W = 0.02 * torch.randn(Cn, E, device=gpu)
     labels = torch.randint(0, Cn, (B,), device=gpu)
+    labels[:ignored] = -100
     dh = torch.zeros(B * S, E, device=gpu)
     gs = torch.tensor([2.0], device=gpu)
-    logits, loss_sum, dW = ops.emotion_head(h, W, labels, B, S, dh=dh, grad_scale=gs)
+    lm = torch.full((B, S), -100, dtype=torch.int64, device=gpu)
+    counts = ops.count_valid(lm, labels, V=100, C_emo=Cn)
+    assert counts.tolist() == [0, B - ignored]
+    logits, loss_sum, dW = ops.emotion_head(h, W, labels, B, S, n_valid=counts[1:], dh=dh, grad_scale=gs)
     hl = h.float().reshape(B, S, E)[:, -1].clone().requires_grad_(True)
     Wr = W.clone().requires_grad_(True)
     ref = hl @ Wr.t()
-    loss = F.cross_entropy(ref, labels)
+    loss = F.cross_entropy(ref, labels, ignore_index=-100)
     (2.0 * loss).backward()
     assert _rel(logits, ref.detach()) < 1e-5
-    assert abs(loss_sum.item() / B - loss.item()) < 1e-5
+    assert abs(loss_sum.item() / (B - ignored) - loss.item()) < 1e-5
     assert _rel(dW, Wr.grad) < 1e-5
     assert _rel(dh.reshape(B, S, E)[:, -1], hl.grad) < 1e-5
     assert torch.all(dh.reshape(B, S, E)[:, :-1] == 0)

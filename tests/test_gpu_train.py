@@ -7,7 +7,7 @@ import tempfile
 import pytest
 import torch
 
-from ergm_amd.config import ERGMConfig
+from ergm_amd.config import ERGMConfig, NO_DROPOUT
 from ergm_amd.dataset import DialogueDataset, PadCollate
 from ergm_amd.model import GPT2LMHeadModel
 from ergm_amd.optim import FusedAdamW, get_polynomial_decay_schedule_with_warmup
@@ -39,7 +39,7 @@ def _data(n_dialogues, seed):
 
 
 def _setup(dev):
-    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=2, n_positions=64)
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=2, n_positions=64, **NO_DROPOUT)
     model = GPT2LMHeadModel(cfg, device=dev)
     model.init_weights(seed=5)
     opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
