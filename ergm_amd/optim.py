@@ -2,9 +2,11 @@
 
 ``FusedAdamW`` is a ``torch.optim.Optimizer`` with torch.optim.AdamW's hyper-parameters, defaults
 and state_dict format (``exp_avg``, ``exp_avg_sq``, ``step`` per parameter), so
-``get_polynomial_decay_schedule_with_warmup`` (src/main.py:93-95) drives it unchanged and checkpoints
-interchange with ``torch.optim.AdamW`` (src/main.py:68,107).  ``step()`` is one HIP launch over the
-flat parameter buffer (``ergm_adamw_step``) that also refreshes the bf16 weight shadow.
+``get_polynomial_decay_schedule_with_warmup`` (src/main.py:93-95) drives it unchanged.  Its one
+parameter is the model's flat fp32 buffer, so its optimizer checkpoints interchange with a
+``torch.optim.AdamW`` built over ``[model.flat]`` — not with the reference's per-tensor AdamW state
+(src/main.py:68,107), whose model part (the state_dict) does interchange.  ``step()`` is one HIP launch
+over the flat parameter buffer (``ergm_adamw_step``) that also refreshes the bf16 weight shadow.
 """
 from __future__ import annotations
 

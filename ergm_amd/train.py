@@ -13,7 +13,9 @@ reference's, so the model part interchanges with reference checkpoints.  They ar
 ``torch.save`` and read back with ``torch.load(weights_only=True)``.
 
 Data parallel: pass a ``process_group``; each rank iterates its own shard (e.g. a
-``DistributedSampler``), and the epoch metrics are summed over ranks before they are reported.
+``DistributedSampler``; every rank must run the same number of steps), the per-step losses are
+already global means (the loss normalisers are all-reduced before each forward), so the epoch loss
+is their rank sum averaged over one rank's steps; correct predictions and samples are summed.
 """
 from __future__ import annotations
 
@@ -71,17 +73,22 @@ class Trainer:
             steps += 1
             samples += kw["input_ids"].shape[0]
         tot = torch.tensor([steps, samples], dtype=torch.float64, device=dev)
+        world = 1
         if self.pg is not None:
             import torch.distributed as dist
+            world = dist.get_world_size(self.pg)
             dist.all_reduce(acc, group=self.pg)
             dist.all_reduce(tot, group=self.pg)
         a, t = acc.tolist(), tot.tolist()
-        n_steps = max(t[0], 1.0)
+        # Under DP each rank's loss is its share of the global step mean (local sums over the global
+        # label counts), so the rank sum is the global mean of one step: divide by the steps one rank
+        # ran (every rank runs the same number), not by the steps summed over ranks.
+        n_steps = max(t[0] / world, 1.0)
         lm = a[1] / n_steps
         ppl = math.exp(lm) if lm < 700 else float("inf")
         if math.isnan(ppl):
             ppl = 1e8  # src/main.py:248-249
-        return EpochStats(loss=a[0] / n_steps, ppl=ppl, acc=100.0 * a[2] / max(t[1], 1.0), steps=int(t[0]),
+        return EpochStats(loss=a[0] / n_steps, ppl=ppl, acc=100.0 * a[2] / max(t[1], 1.0), steps=int(n_steps),
                           samples=int(t[1]))
 
     def train_epoch(self, loader) -> EpochStats:

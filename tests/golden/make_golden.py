@@ -9,10 +9,15 @@ as ``tests/golden/*.npz``.  Also pins the AdamW / LR-schedule restatement agains
 ``torch.optim.AdamW`` + ``transformers.get_polynomial_decay_schedule_with_warmup`` (the third-party
 code src/main.py:68,93-95 calls).
 
-Usage:  python tests/golden/make_golden.py
+Also captures, from the reference's own code: the 2-D ``imgs`` semantics (src/model.py:497), the
+data pipeline (``CustomDataset`` + ``PadCollate``, src/custom_dataset.py) on synthetic pickles, and
+three steps of the src/main.py training loop with its reported metrics.
+
+Usage:  python tests/golden/make_golden.py [--only imgs2d,dataset,trainer]
 """
 from __future__ import annotations
 
+import json
 import os
 import sys
 import types
@@ -194,10 +199,197 @@ def adamw_case():
     return rec
 
 
+def imgs2d_case(refmodel):
+    """The reference's imgs[i][0] (src/model.py:497) on a 2-D [B, E] ``imgs`` tensor: the SCALAR
+    imgs[i, 0], broadcast over position 0's embedding (vs row 0 of a 3-D tensor)."""
+    cfg = O.OracleConfig(vocab_size=256, n_embd=64, n_layer=2, n_head=1, n_positions=64)
+    seed = 55
+    print(f"[imgs2d_e64] 2-D imgs, L={cfg.n_layer} E={cfg.n_embd}")
+    P = O.init_params(cfg, seed=seed)
+    batch = synthetic_batch(2, 32, n_turns=3, feat_dim=cfg.n_embd, seed=seed + 1000, vocab_hi=253, sp1=254,
+                            sp2=255, eos=252)
+    imgs = batch.pop("visual_feat")[:, 0].contiguous()   # [B, E]
+    from transformers import GPT2Config
+    gcfg = GPT2Config(vocab_size=cfg.vocab_size, n_embd=cfg.n_embd, n_layer=cfg.n_layer, n_head=cfg.n_head,
+                      n_positions=cfg.n_positions, attn_pdrop=0.0, resid_pdrop=0.0, embd_pdrop=0.0)
+    net = refmodel.GPT2LMHeadModel(gcfg)
+    sd = dict(P)
+    sd["lm_head.weight"] = P["transformer.wte.weight"]
+    net.load_state_dict(sd, strict=True)
+    net.train()
+    out = net(input_ids=batch["input_ids"], token_type_ids=batch["token_type_ids"], labels=batch["labels"],
+              emotion_labels=batch["emotion_labels"], caption_ids=batch["caption_ids"], imgs=imgs,
+              auds=batch["audio_feat"])
+    out.loss.backward()
+    ref_g = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+    ora, og = O.loss_and_grads(P, cfg, dict(batch, imgs=imgs))
+    ok = compare("loss", ora["loss"].reshape(1), out.loss.detach().reshape(1), 1e-5)
+    ok &= compare("logits", ora["logits"], out.logits.detach(), 1e-5)
+    for k in og:
+        ok &= compare("grad " + k, og[k], ref_g[k], 1e-4)
+    vec, _ = O.loss_and_grads(P, cfg, dict(batch, visual_feat=imgs))
+    assert abs(vec["loss"].item() - out.loss.item()) > 1e-6, "2-D imgs must differ from the vector form"
+    assert ok
+    rec = {"config": np.array([cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_positions]),
+           "seed": np.array(seed), "loss": out.loss.detach().numpy(), "logits": out.logits.detach().numpy(),
+           "emotion_logits": out.emotion_logits.detach().numpy(), "in_imgs": imgs.numpy()}
+    for k, v in batch.items():
+        rec["in_" + k] = v.numpy()
+    for k, g in ref_g.items():
+        rec["grad:" + k] = g.numpy()
+    return rec
+
+
+def dataset_case():
+    """The reference's CustomDataset + PadCollate (src/custom_dataset.py:9-132) on synthetic pickles of
+    the reference schema.  The reference keeps only the first dialogue of a file (its debugging
+    ``[:1]`` slices, :21,27), so each dialogue is written to its own pair of pickles and the reference
+    dataset is built once per dialogue; the concatenated samples are what a full run (slices removed,
+    as its comment instructs) yields — the build's DialogueDataset processes every dialogue."""
+    import pickle
+    import tempfile
+    from argparse import Namespace
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    import custom_dataset as refds
+    g = torch.Generator().manual_seed(77)
+    eos, sp1, sp2, Fd = 50256, 50258, 50259, 8
+
+    def toks(n):
+        return torch.randint(0, 50257, (n,), generator=g).tolist()
+    dialogues = []
+    for i, shapes in enumerate([[(3, [5, 4, 6]), (4, [3, 3, 2, 7])], [(2, [9, 3])], [(2, [700, 400]), (1, [12])]]):
+        txt, tgt, ctx, emo = [], [], [], []
+        for j, (nt, lens) in enumerate(shapes):
+            turns = [toks(n) for n in lens]
+            txt.append(turns)
+            # target lengths: shorter than, longer than and (the 1100-token utterance aside) like the input
+            tl = {0: sum(lens) // 2, 1: sum(lens) + 5}.get((i + j) % 3, sum(lens) - 1)
+            tgt.append([50257, sp1] + toks(max(tl, 1)) + [eos, eos])
+            ctx.append(toks(6 + j))
+            emo.append((3 * i + j) % 7)
+        img = [torch.randn(Fd, generator=g).tolist()]
+        aud = [torch.randn(Fd, generator=g).tolist()]
+        dialogues.append(({"txt": [txt], "img": [img], "aud": [aud], "label": [tgt]},
+                          {"context": [ctx], "label": [emo]}))
+    samples = []
+    tmp = tempfile.mkdtemp(prefix="ergm_ds_")
+    for data, cl in dialogues:
+        with open(os.path.join(tmp, "multi_train_data.pkl"), "wb") as f:
+            pickle.dump(data, f)
+        with open(os.path.join(tmp, "context_label_train_data.pkl"), "wb") as f:
+            pickle.dump(cl, f)
+        args = Namespace(train_prefix="train", valid_prefix="valid", data_dir=tmp, sp1_id=sp1, sp2_id=sp2, eos_id=eos)
+        ds = refds.CustomDataset("train", args)
+        samples += [ds[k] for k in range(len(ds))]
+    collate = refds.PadCollate(eos, Namespace())
+    batches = [collate.pad_collate(samples), collate.pad_collate(samples[1:3])]
+    n = len(samples)
+    Smax = max(len(x[0]) for x in samples)
+    rec = {"n": np.array(n), "eos": np.array(eos), "sp1": np.array(sp1), "sp2": np.array(sp2),
+           "lengths": np.array([len(x[0]) for x in samples]),
+           "emotion": np.array([x[6] for x in samples]),
+           "img0": np.array([x[3][0] for x in samples], dtype=np.float32),
+           "aud0": np.array([x[4][0] for x in samples], dtype=np.float32),
+           "n_img_rows": np.array([len(x[3]) for x in samples])}
+    for key, col in (("input_ids", 0), ("token_type_ids", 1), ("labels", 2)):
+        a = np.full((n, Smax), -7, dtype=np.int64)  # -7: beyond the sample
+        for r, x in enumerate(samples):
+            a[r, :len(x[col])] = x[col]
+        rec["sample_" + key] = a
+    ctx_len = max(len(x[5]) for x in samples)
+    c = np.full((n, ctx_len), -7, dtype=np.int64)
+    for r, x in enumerate(samples):
+        c[r, :len(x[5])] = x[5]
+    rec["sample_context"] = c
+    for bi, b in enumerate(batches):
+        for key, col in (("input_ids", 0), ("token_type_ids", 1), ("labels", 2)):
+            rec[f"batch{bi}_" + key] = b[col].numpy()
+    # the raw dialogues (the restatement's input)
+    for i, (data, cl) in enumerate(dialogues):
+        rec[f"dlg{i}_json"] = np.frombuffer(json.dumps({"data": data, "cl": cl}).encode(), dtype=np.uint8)
+    print(f"  reference dataset: {n} samples from {len(dialogues)} dialogues (utterances >= 1024 tokens skipped)")
+    return rec
+
+
+def trainer_case(refmodel):
+    """Three reference training steps of src/main.py's loop (:137-169: forward, zero_grad, backward,
+    AdamW step, scheduler step, loss.item(), the no-grad LM cross-entropy over the logits, emotion
+    argmax accuracy) with the poly-decay schedule (:93-95), then the epoch metrics (:171-176:
+    mean loss, PPL = exp(mean LM loss), accuracy in %) and a validation pass (:206-251)."""
+    import math
+    import torch.nn as nn
+    from transformers import GPT2Config, get_polynomial_decay_schedule_with_warmup
+    cfg = O.OracleConfig(vocab_size=256, n_embd=64, n_layer=2, n_head=1, n_positions=64)
+    seed = 66
+    P = O.init_params(cfg, seed=seed)
+    gcfg = GPT2Config(vocab_size=cfg.vocab_size, n_embd=cfg.n_embd, n_layer=cfg.n_layer, n_head=cfg.n_head,
+                      n_positions=cfg.n_positions, attn_pdrop=0.0, resid_pdrop=0.0, embd_pdrop=0.0)
+    net = refmodel.GPT2LMHeadModel(gcfg)
+    sd = dict(P)
+    sd["lm_head.weight"] = P["transformer.wte.weight"]
+    net.load_state_dict(sd, strict=True)
+    lr, steps = 1e-3, 3
+    optim = torch.optim.AdamW(net.parameters(), lr=lr)
+    sched = get_polynomial_decay_schedule_with_warmup(optim, num_warmup_steps=1, num_training_steps=steps, power=2)
+    batches = [synthetic_batch(8, 16, n_turns=2, feat_dim=cfg.n_embd, seed=seed + 10 + k, vocab_hi=253, sp1=254,
+                               sp2=255, eos=252) for k in range(steps + 1)]
+    net.train()
+    losses, lm_losses, correct, total = [], [], 0, 0
+    for b in batches[:steps]:
+        out = net(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], labels=b["labels"],
+                  emotion_labels=b["emotion_labels"], caption_ids=b["caption_ids"], imgs=b["visual_feat"],
+                  auds=b["audio_feat"])
+        loss = out.loss
+        optim.zero_grad()
+        loss.backward()
+        optim.step()
+        sched.step()
+        losses.append(loss.item())
+        with torch.no_grad():
+            sl = out.logits[..., :-1, :].contiguous()
+            lab = b["labels"][..., 1:].contiguous()
+            lm_losses.append(nn.CrossEntropyLoss()(sl.view(-1, sl.size(-1)), lab.view(-1)).item())
+            correct += (torch.argmax(out.emotion_logits, dim=-1) == b["emotion_labels"]).sum().item()
+            total += b["emotion_labels"].size(0)
+    train = [float(np.mean(losses)), math.exp(float(np.mean(lm_losses))), correct / total * 100]
+    net.eval()
+    with torch.no_grad():
+        b = batches[steps]
+        out = net(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], labels=b["labels"],
+                  emotion_labels=b["emotion_labels"], caption_ids=b["caption_ids"], imgs=b["visual_feat"],
+                  auds=b["audio_feat"])
+        sl = out.logits[..., :-1, :].contiguous()
+        lab = b["labels"][..., 1:].contiguous()
+        vlm = nn.CrossEntropyLoss()(sl.view(-1, sl.size(-1)), lab.view(-1)).item()
+        vacc = (torch.argmax(out.emotion_logits, dim=-1) == b["emotion_labels"]).sum().item() / 8 * 100
+        margins = out.emotion_logits.topk(2, dim=-1).values
+        valid = [out.loss.item(), math.exp(vlm), vacc]
+    print(f"  reference loop: train loss/ppl/acc {train}, valid {valid}")
+    rec = {"config": np.array([cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_positions]),
+           "seed": np.array(seed), "lr": np.array(lr), "steps": np.array(steps),
+           "step_losses": np.array(losses), "step_lm_losses": np.array(lm_losses),
+           "train_metrics": np.array(train), "valid_metrics": np.array(valid),
+           "valid_emotion_margin": (margins[:, 0] - margins[:, 1]).numpy()}
+    for k, b in enumerate(batches):
+        for n, v in b.items():
+            rec[f"b{k}_{n}"] = v.numpy()
+    return rec
+
+
 def main():
     torch.manual_seed(0)
     refmodel = load_reference()
     out_dir = HERE
+    if "--only" in sys.argv:  # regenerate selected new fixtures without rewriting the older ones
+        only = sys.argv[sys.argv.index("--only") + 1].split(",")
+        cases = {"imgs2d": ("imgs2d_e64.npz", lambda: imgs2d_case(refmodel)),
+                 "dataset": ("dataset_ref.npz", dataset_case),
+                 "trainer": ("trainer_ref.npz", lambda: trainer_case(refmodel))}
+        for c in only:
+            fn, make = cases[c]
+            np.savez_compressed(os.path.join(out_dir, fn), **make())
+        return
     # 1. tiny, single head (d=64), full grads + one AdamW step: the byte-level fixture
     cfg = O.OracleConfig(vocab_size=256, n_embd=64, n_layer=2, n_head=1, n_positions=64)
     P, batch, rec = build_case(refmodel, "tiny_e64", cfg, B=2, S=32, seed=11)
@@ -217,6 +409,10 @@ def main():
                            full_grads=False, vocab_hi=50257)
     np.savez_compressed(os.path.join(out_dir, "c2slice_gpt2small_fusion.npz"), **rec)
     np.savez_compressed(os.path.join(out_dir, "adamw_sched.npz"), **adamw_case())
+    # 5. 2-D imgs (scalar imgs[i][0]), 6. the reference data pipeline, 7. the reference train loop's metrics
+    np.savez_compressed(os.path.join(out_dir, "imgs2d_e64.npz"), **imgs2d_case(refmodel))
+    np.savez_compressed(os.path.join(out_dir, "dataset_ref.npz"), **dataset_case())
+    np.savez_compressed(os.path.join(out_dir, "trainer_ref.npz"), **trainer_case(refmodel))
     print("golden fixtures written to", out_dir)
 
 

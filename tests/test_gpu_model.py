@@ -326,3 +326,37 @@ def test_odd_token_counts_match_oracle(gpu, B, S, feat):
     assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
     assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
     _grad_gate(_grads(model), og)
+
+
+def test_two_dimensional_imgs_match_reference_golden(gpu):
+    """``imgs`` as a 2-D [B, E] tensor: the reference adds imgs[i][0] — the scalar imgs[i, 0] —
+    to position 0 (src/model.py:497); golden imgs2d_e64.npz is the reference's own output."""
+    rec = _load("imgs2d_e64.npz")
+    ocfg, cfg, P0, model, batch = _setup(rec, gpu)
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    model.flat.grad = None
+    out = model(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["imgs"],
+                auds=kw["audio_feat"])
+    out.loss.backward()
+    torch.cuda.synchronize()
+    ref_loss = float(rec["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    assert (out.logits.float().cpu() - torch.from_numpy(rec["logits"])).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), {k: rec["grad:" + k] for k in _grads(model)})
+
+
+def test_second_forward_before_backward_raises(gpu):
+    """One set of saved activations per (batch, seq) shape: differentiating a training forward after
+    another forward of the same shape overwrote them raises instead of silently using the second
+    batch (gradient accumulation must call backward per micro-batch)."""
+    rec = _load("tiny_e64.npz")
+    _, _, _, model, batch = _setup(rec, gpu)
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    args = dict(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+                auds=kw["audio_feat"])
+    o1 = model(**args)
+    o2 = model(**args)
+    with pytest.raises(RuntimeError, match="overwrote"):
+        (o1.loss + o2.loss).backward()

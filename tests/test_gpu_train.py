@@ -83,3 +83,42 @@ def test_trainer_epochs_checkpoint_and_resume(gpu):
     assert torch.equal(m3.flat, m1.flat)
     assert again.loss == first.loss and again.acc == first.acc
     assert va.loss < v0.loss  # training reduced the validation loss
+
+
+def test_trainer_metrics_match_reference_loop(gpu):
+    """Trainer's reported epoch metrics against three steps of the reference's own training loop
+    (src/main.py:137-176: loss.item() mean, PPL = exp(mean of the no-grad LM cross-entropy over the
+    logits), emotion argmax accuracy; AdamW + poly-decay schedule) and one validation pass
+    (:206-251), captured by tests/golden/make_golden.py (trainer_ref.npz).  bf16 gates: per-step loss
+    rel 2e-3 (the later steps follow three bf16 AdamW updates), PPL rel 2e-2, accuracy within one
+    sample per near-tie."""
+    import math
+    import numpy as np
+    from oracle import gpt2_oracle as O
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trainer_ref.npz"))
+    Vr, Er, Lr, Hr, Pr = (int(x) for x in z["config"])
+    cfg = ERGMConfig(vocab_size=Vr, n_embd=Er, n_layer=Lr, n_head=Hr, n_positions=Pr, **NO_DROPOUT)
+    steps = int(z["steps"])
+    batches = []
+    k = 0
+    while f"b{k}_input_ids" in z:
+        batches.append({n[len(f"b{k}_"):]: torch.from_numpy(z[n]) for n in z.files if n.startswith(f"b{k}_")})
+        k += 1
+    P0 = O.init_params(O.OracleConfig(vocab_size=Vr, n_embd=Er, n_layer=Lr, n_head=Hr, n_positions=Pr),
+                       seed=int(z["seed"]))
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    opt = FusedAdamW([model.flat], lr=float(z["lr"]), model=model, overlap=True)
+    sched = get_polynomial_decay_schedule_with_warmup(opt, 1, steps, power=2)
+    tr = Trainer(model, opt, sched)
+    got = tr.train_epoch(batches[:steps])
+    want = z["train_metrics"]
+    assert got.steps == steps and got.samples == 8 * steps
+    assert abs(got.loss - want[0]) <= 2e-3 * abs(want[0]), (got, want)
+    assert abs(got.ppl - want[1]) <= 2e-2 * abs(want[1]), (got, want)
+    assert abs(got.acc - want[2]) <= 100.0 / (8 * steps) + 1e-9, (got, want)
+    va = tr.validation(batches[steps:])
+    vw = z["valid_metrics"]
+    assert abs(va.loss - vw[0]) <= 2e-3 * abs(vw[0]) and abs(va.ppl - vw[1]) <= 2e-2 * abs(vw[1]), (va, vw)
+    near_ties = int((z["valid_emotion_margin"] < 2e-2).sum())
+    assert abs(va.acc - vw[2]) <= 100.0 * near_ties / 8 + 1e-9, (va, vw, near_ties)
