@@ -167,6 +167,8 @@ def main():
     ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
+    ap.add_argument("--pdrop", type=float, default=None,
+                    help="attn/resid/embd dropout (default: the config's 0.1, as the reference trains; 0 = off)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -221,6 +223,8 @@ def main():
     if not fp8:
         desc = desc.replace("fp8 (e4m3) forward Conv1D GEMMs", "bf16 GEMMs")
     cfg = ERGMConfig(**MODELS[mname], feat_dim=Fd, fp8=fp8)
+    if args.pdrop is not None:
+        cfg.attn_pdrop = cfg.resid_pdrop = cfg.embd_pdrop = args.pdrop
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
@@ -317,6 +321,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp8e4m3 fwd GEMMs + bf16" if fp8 else "bf16",
+        "dropout": {"attn": cfg.attn_pdrop, "resid": cfg.resid_pdrop, "embd": cfg.embd_pdrop, "mode": "train"},
         "data": f"synthetic (seeded MELD-shape token/feature batches; random-init GPT-2-{mname} weights)",
         "config": {"workload": desc, "model": f"GPT-2-{mname} (L={Lyr}, E={E}, H={cfg.n_head}, V={V}) + "
                    "cross-attention caption fusion + emotion head", "global_batch": B * world, "seq_len": S,

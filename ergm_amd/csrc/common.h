@@ -89,6 +89,15 @@ __device__ __forceinline__ float gelu_new(float x) {
     float u = k0 * (x + 0.044715f * x * x * x);
     return 0.5f * x * (1.0f + tanhf(u));
 }
+// gelu_new(x) and its derivative from one tanh: the forward keeps the derivative for the backward
+// (the GELU backward is then a plain product, no transcendental on the backward critical path)
+__device__ __forceinline__ float gelu_new_fwd(float x, float& dgelu) {
+    const float k0 = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float t = tanhf(k0 * (x + 0.044715f * x2 * x));
+    dgelu = 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * 0.044715f * x2);
+    return 0.5f * x * (1.0f + t);
+}
 __device__ __forceinline__ float gelu_new_grad(float x) {
     const float k0 = 0.7978845608028654f;
     float x2 = x * x;

@@ -51,15 +51,14 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
         if (a.bias) v += a.bias[n];
     }
     if (EPI == ERGM_EPI_BIAS_GELU) {
-        __bf16 pre = f2bf(v);
-        reinterpret_cast<__bf16*>(a.aux_out)[(size_t)m * a.ld_aux_out + n] = pre;
-        v = gelu_new(v);
+        float dg;
+        v = gelu_new_fwd(v, dg);
+        reinterpret_cast<__bf16*>(a.aux_out)[(size_t)m * a.ld_aux_out + n] = f2bf(dg);
     } else if (EPI == ERGM_EPI_BIAS_RESID) {
         if (a.drop.thresh) v = drop_keep1(a.drop, m, n) ? v * a.drop.scale : 0.f;
         v += reinterpret_cast<const float*>(a.aux)[(size_t)m * a.ld_aux + n];
     } else if (EPI == ERGM_EPI_GELU_BWD) {
-        float x = bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);
-        v *= gelu_new_grad(x);
+        v *= bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);  // stored gelu'(pre)
     }
     size_t idx = (size_t)m * a.ldc + n;
     if (OUT_BF16) {
@@ -82,14 +81,15 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
             v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
     }
-    if (EPI == ERGM_EPI_BIAS_GELU) {
-        bf16x8 pre;
+    if (EPI == ERGM_EPI_BIAS_GELU) {  // C = gelu_new(v), aux_out = gelu_new'(v) for the backward
+        bf16x8 dgb;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            pre[j] = f2bf(v[j]);
-            v[j] = gelu_new(v[j]);
+            float dg;
+            v[j] = gelu_new_fwd(v[j], dg);
+            dgb[j] = f2bf(dg);
         }
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.aux_out) + (size_t)m * a.ld_aux_out + n) = pre;
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.aux_out) + (size_t)m * a.ld_aux_out + n) = dgb;
     } else if (EPI == ERGM_EPI_BIAS_RESID) {
         if (a.drop.thresh) {  // residual-branch dropout, then the residual add
             const unsigned k = drop_keep4(a.drop, m, n) | (drop_keep4(a.drop, m, n + 4) << 4);
@@ -100,10 +100,10 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
         float4 r0 = *reinterpret_cast<const float4*>(r), r1 = *reinterpret_cast<const float4*>(r + 4);
         v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
-    } else if (EPI == ERGM_EPI_GELU_BWD) {
+    } else if (EPI == ERGM_EPI_GELU_BWD) {  // v · gelu_new'(pre), the derivative stored by the forward
         bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.aux) + (size_t)m * a.ld_aux + n);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_new_grad(bf2f(x[j]));
+        for (int j = 0; j < 8; ++j) v[j] *= bf2f(x[j]);
     }
     const size_t idx = (size_t)m * a.ldc + n;
     if (OUT_BF16) {

@@ -53,7 +53,7 @@ int proj_grad_pack(const float* dh0, void* d, int B, int Bp, int S, int E, hipSt
 struct LayerActs {
     __bf16 *ln1, *lnx, *ln2;
     float *m1, *r1, *mx, *rx, *m2, *r2;
-    __bf16 *qkv, *ao, *xq, *xo, *pre, *act;
+    __bf16 *qkv, *ao, *xq, *xo, *pre, *act;  // pre: gelu_new' of the c_fc pre-activation (GELU backward factor)
     float *lse, *xlse;
 };
 
@@ -105,8 +105,11 @@ struct ergm_model_plan {
     // of stage l (ergm_model_backward_layer's ordering guarantee); 0 = only the embedding stage joins,
     // consumers of a block's gradients wait with ergm_model_stage_wait instead
     bool per_stage_join;
-    // forward batch-half chains: the second runs on fwd2 (ev_f2: fork, embedding done, chain done)
-    int fwd_chains;
+    // forward batch-half chains: the second runs on fwd2 (ev_f2: fork, embedding done, chain done);
+    // the backward's data-gradient chains likewise (bwd_forked: the second chain is running, forked
+    // after the head stage and joined by the embedding stage)
+    int fwd_chains, bwd_chains;
+    bool bwd_forked;
     hipStream_t fwd2;
     hipEvent_t ev_f2[3];
     char* scratch3;
@@ -355,6 +358,34 @@ int fork_side(ergm_model_plan* P, hipStream_t s) {
     return ERGM_OK;
 }
 
+// The backward's data-gradient chains: every kernel of a block's data-gradient path is row- (or
+// batch-) separable, so like the forward it runs as two concurrent chains over the two halves of the
+// batch (the caller's stream and P->fwd2) and writes disjoint rows of the same buffers; the weight-
+// gradient GEMMs (side stream, contraction over all tokens) wait for both.  One chain when the batch
+// does not split into halves whose token counts are multiples of the LayerNorm-backward partial block.
+struct Chains {
+    int n;
+    hipStream_t s[2];
+    int b0[2], nb[2];
+};
+Chains bwd_chains(const ergm_model_plan* P, hipStream_t s) {
+    Chains c{};
+    const int B = P->d.batch, S = P->d.seq;
+    const bool two = !P->dry && P->bwd_chains >= 2 && B >= 2 && ((B / 2) * S) % 8 == 0;
+    c.n = two ? 2 : 1;
+    c.s[0] = s;
+    c.s[1] = two ? P->fwd2 : s;
+    c.b0[0] = 0;
+    c.nb[0] = two ? B / 2 : B;
+    c.b0[1] = c.nb[0];
+    c.nb[1] = B - c.nb[0];
+    return c;
+}
+int fork_side(ergm_model_plan* P, const Chains& c) {
+    for (int i = 0; i < c.n; ++i) ERGM_TRY(fork_side(P, c.s[i]));
+    return ERGM_OK;
+}
+
 // Record stage event `k` on the side stream / make `s` wait for a recorded stage event.
 int side_mark(ergm_model_plan* P, int k) {
     if (P->dry) return ERGM_OK;
@@ -365,39 +396,52 @@ int join_side(ergm_model_plan* P, hipStream_t s, int k) {
     return hipStreamWaitEvent(s, P->ev_join[k], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: stream join");
 }
 
-int dw_gemm(ergm_model_plan* P, hipStream_t s_main, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
+int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB) {
     const int T = P->T;
-    ERGM_TRY(fork_side(P, s_main));
-    hipStream_t s = P->dry ? s_main : P->side;
+    ERGM_TRY(fork_side(P, ch));
+    hipStream_t s = P->dry ? ch.s[0] : P->side;
     if (P->fused_bias)
         return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
     ERGM_TRY(gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE));
     return colsum(P, s, dY, ERGM_BF16, T, N, ldy, gB);
 }
 
-// LayerNorm backward on the critical chain; its dγ/dβ partials go to a per-LN slot (nothing later
-// overwrites them) and are reduced on the side stream: by ln_reduce_flush, which batches the pending
-// LayerNorms of a block into one launch.
-int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
-           float* dgamma, float* dbeta, __bf16* dh_b, int slot) {
+// LayerNorm backward on the critical chain(s): rows [r0, r0 + rows) of the residual stream; its dγ/dβ
+// partials (one per 8-row block, so every chain writes its own partial rows and the reduce sees the
+// one-chain partials bit for bit) go to a per-LN slot (nothing later overwrites them) and are reduced
+// on the side stream by ln_reduce_flush, which batches the pending LayerNorms of a block into one launch.
+int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd,
+                const float* gamma, __bf16* dh_b, int slot, int r0, int rows) {
     if (P->dry) return ERGM_OK;
     const int T = P->T, E = P->d.n_embd;
     float* pg = P->ln_part[slot];
     float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
+    const size_t o = (size_t)r0 * E, po = (size_t)(r0 / 8) * E;
     // dh_b feeds the residual branch that produced this residual-stream tensor (slot = its index):
     // through that branch's dropout (slot 0, the embeddings: unused by any GEMM)
-    const ergm_dropout dd = resid_drop(P, slot, 0);
-    ERGM_TRY(layernorm_bwd_main(P->dy, x, mean, rstd, gamma, P->dh, dh_b, pg, pb, T, E, s, drop_site_of(&dd, E)));
+    const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
+    return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, dh_b + o, pg + po, pb + po, rows,
+                              E, s, drop_site_of(&dd, E));
+}
+int ln_reduce_add(ergm_model_plan* P, int slot, float* dgamma, float* dbeta) {
+    if (P->dry) return ERGM_OK;
     ERGM_CHECK_ARG(P->ln_pending < 4, "model: too many pending LayerNorm reductions");
+    float* pg = P->ln_part[slot];
     const int k = P->ln_pending++;
-    P->lnr_pg[k] = pg; P->lnr_pb[k] = pb; P->lnr_dg[k] = dgamma; P->lnr_db[k] = dbeta;
+    P->lnr_pg[k] = pg; P->lnr_pb[k] = pg + (size_t)ln_bwd_nparts(P->T) * P->d.n_embd;
+    P->lnr_dg[k] = dgamma; P->lnr_db[k] = dbeta;
     return ERGM_OK;
 }
+int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean, const float* rstd, const float* gamma,
+           float* dgamma, float* dbeta, __bf16* dh_b, int slot) {
+    ERGM_TRY(ln_bwd_rows(P, s, x, mean, rstd, gamma, dh_b, slot, 0, P->T));
+    return ln_reduce_add(P, slot, dgamma, dbeta);
+}
 
-int ln_reduce_flush(ergm_model_plan* P, hipStream_t s) {
+int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
     if (P->dry || P->ln_pending == 0) return ERGM_OK;
-    ERGM_TRY(fork_side(P, s));
+    ERGM_TRY(fork_side(P, ch));
     const int n = P->ln_pending;
     P->ln_pending = 0;
     return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
@@ -522,6 +566,11 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     // ERGM_FWD_CHAINS=1 disables the two-chain forward (A/B measurements)
     P->fwd_chains = 2;
     if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = atoi(e);
+    // two backward chains measured slower at C2 (6.27 vs 5.85 ms/step: the GPU is already throughput-
+    // saturated and the host enqueue grows, profiles/r02_bwd_chains_ab.txt): ERGM_BWD_CHAINS=2 enables
+    P->bwd_chains = 1;
+    if (const char* e = getenv("ERGM_BWD_CHAINS")) P->bwd_chains = atoi(e);
+    P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
     for (auto& e : P->ev_f2) e = nullptr;
@@ -916,6 +965,7 @@ namespace {
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     P->ln_pending = 0;
+    P->bwd_forked = false;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad, L = d.n_layer;
     // dh_f = dlogits · wte (contraction over the padded vocab) on the main chain; the tied-weight
@@ -947,8 +997,14 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
 
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     const ergm_model_dims& d = P->d;
-    const int T = P->T, E = d.n_embd, F = d.n_inner, H = d.n_head, B = d.batch, S = d.seq, L2E = P->L2E;
+    const int E = d.n_embd, F = d.n_inner, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int L = d.n_layer;
+    const Chains ch = bwd_chains(P, s);
+    if (ch.n == 2 && !P->bwd_forked) {  // the second chain starts from the head stage's outputs
+        if (hipEventRecord(P->ev_f2[0], s) != hipSuccess || hipStreamWaitEvent(P->fwd2, P->ev_f2[0], 0) != hipSuccess)
+            return fail(ERGM_EHIP, "model: backward chain fork");
+        P->bwd_forked = true;
+    }
     LayerActs a = P->dry ? LayerActs{} : P->la[l];
     const float* x0 = P->dry ? nullptr : P->resid[3 * l];
     const float* x1 = P->dry ? nullptr : P->resid[3 * l + 1];
@@ -960,49 +1016,70 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     __bf16* dpre = P->dpre[l];
     __bf16* dxq = P->dxq[l];
     __bf16* dqkv = P->dqkv[l];
-    // ---- MLP: x3 = x2 + gelu(ln2(x2)·Wfc + bfc)·Wm + bm
-    ERGM_TRY(dw_gemm(P, s, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
-    ERGM_TRY(gemm(P, s, T, F, E, dh3, E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK, dpre, F, ERGM_BF16,
-                  ERGM_EPI_GELU_BWD, nullptr, a.pre, F));
-    ERGM_TRY(dw_gemm(P, s, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
-    ERGM_TRY(gemm(P, s, T, E, F, dpre, F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK, P->dy, E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B), dh2,
-                    3 * l + 2));
-    // ---- cross-attention: x2 = x1 + Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp
-    ERGM_TRY(dw_gemm(P, s, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, dh2, E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
-                  ERGM_EPI_NONE));
-    if (!P->dry) {
-        const __bf16* kl = P->kv_all + (size_t)l * 2 * E;
-        __bf16* dkl = P->dkv_all + (size_t)l * 2 * E;
-        const ergm_dropout dp = attn_drop(P, l, 1, 0);
-        ERGM_TRY(ergm_attn_bwd(a.xq, kl, kl + E, a.xo, P->d_o, a.xlse, P->delta, dxq, dkl, dkl + E, B, H, S, S, E,
-                               L2E, L2E, P->XE, E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, 0), s));
+    // per-chain row offset helpers (dry run: pointers stay null)
+    auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
+    auto Tc = [&](int c) { return ch.nb[c] * S; };
+    auto lnrow = [&](const float* p, int c) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S; };
+    // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
+    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
+    for (int c = 0; c < ch.n; ++c)
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
+                      R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
+    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
+    for (int c = 0; c < ch.n; ++c) {
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
+                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     }
-    ERGM_TRY(dw_gemm(P, s, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, dxq, E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK, P->dy, E, ERGM_F32,
-                  ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B), dh1,
-                    3 * l + 1));
-    // ---- self-attention: x1 = x0 + Attn(ln_1(x0)·Wqkv + b)·Wap + bap
-    ERGM_TRY(dw_gemm(P, s, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
-    ERGM_TRY(gemm(P, s, T, E, E, dh1, E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK, P->d_o, E, ERGM_BF16,
-                  ERGM_EPI_NONE));
-    if (!P->dry) {
-        const ergm_dropout dp = attn_drop(P, l, 0, 0);
-        ERGM_TRY(ergm_attn_bwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, P->d_o, a.lse, P->delta, dqkv, dqkv + E,
-                               dqkv + 2 * E, B, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E, 3 * E, 3 * E, 1, &dp,
-                               attn_bits(P, l, 0, 0), s));
+    ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
+    // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
+    for (int c = 0; c < ch.n; ++c) {
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
+                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (!P->dry) {
+            const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
+            __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
+            const ergm_dropout dp = attn_drop(P, l, 1, ch.b0[c]);
+            const size_t bhs = (size_t)ch.b0[c] * H * S;
+            ERGM_TRY(ergm_attn_bwd(R(a.xq, c, E), kl, kl + E, R(a.xo, c, P->XE), R(P->d_o, c, E), a.xlse + bhs,
+                                   P->delta + bhs, R(dxq, c, E), dkl, dkl + E, ch.nb[c], H, S, S, E, L2E, L2E, P->XE,
+                                   E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, ch.b0[c]), ch.s[c]));
+        }
     }
-    ERGM_TRY(dw_gemm(P, s, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
-    ERGM_TRY(gemm(P, s, T, E, 3 * E, dqkv, 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_NK, P->dy, E,
-                  ERGM_F32, ERGM_EPI_NONE));
-    ERGM_TRY(ln_bwd(P, s, x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B), dh0,
-                    3 * l));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
+    for (int c = 0; c < ch.n; ++c) {
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
+                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
+    }
+    ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
+    // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
+    for (int c = 0; c < ch.n; ++c) {
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
+                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (!P->dry) {
+            const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
+            const size_t bhs = (size_t)ch.b0[c] * H * S;
+            const __bf16* q = R(a.qkv, c, 3 * E);
+            __bf16* dq = R(dqkv, c, 3 * E);
+            ERGM_TRY(ergm_attn_bwd(q, q + E, q + 2 * E, R(a.ao, c, P->XE), R(P->d_o, c, E), a.lse + bhs, P->delta + bhs,
+                                   dq, dq + E, dq + 2 * E, ch.nb[c], H, S, S, 3 * E, 3 * E, 3 * E, P->XE, E, 3 * E,
+                                   3 * E, 3 * E, 1, &dp, attn_bits(P, l, 0, ch.b0[c]), ch.s[c]));
+        }
+    }
+    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
+    for (int c = 0; c < ch.n; ++c) {
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
+                      ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
+    }
+    ERGM_TRY(ln_reduce_add(P, 3 * l, LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B)));
+    (void)lnrow;
     // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
     // those of the block differentiated before, so block l+1's gradients are final on return.
-    ERGM_TRY(ln_reduce_flush(P, s));  // this block's three LayerNorms (+ ln_f after the head stage)
+    ERGM_TRY(ln_reduce_flush(P, ch));  // this block's three LayerNorms (+ ln_f after the head stage)
     ERGM_TRY(side_mark(P, l));
     if (l + 1 < L && P->per_stage_join) ERGM_TRY(join_side(P, s, l + 1));
     return ERGM_OK;
@@ -1012,6 +1089,12 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, L2E = P->L2E, L = d.n_layer;
+    if (P->bwd_forked) {  // the second backward chain's rows of dh are final: join it
+        if (hipEventRecord(P->ev_f2[2], P->fwd2) != hipSuccess || hipStreamWaitEvent(s, P->ev_f2[2], 0) != hipSuccess)
+            return fail(ERGM_EHIP, "model: backward chain join");
+        P->bwd_forked = false;
+    }
+    const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
     if (!P->dry) {  // dh = gradient of the dropped embedding sum: through the embedding dropout (src/model.py:506)
         const ergm_dropout de = resid_drop(P, 0, 0);
         ERGM_TRY(dropout_apply_f32(drop_site_of(&de, E), P->dh, T, E, E, s));
@@ -1037,7 +1120,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
         }
     }
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
-    ERGM_TRY(dw_gemm(P, s, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
+    ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
     ERGM_TRY(side_mark(P, L + 2));
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));

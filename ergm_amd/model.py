@@ -31,9 +31,10 @@ activations per shape).
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -73,54 +74,113 @@ def _as_config(config) -> ERGMConfig:
                       embd_pdrop=g("embd_pdrop", 0.1))
 
 
-class _FusedTrainStep(torch.autograd.Function):
-    """Autograd bridge: forward = one native forward; backward = native backward stages writing
-    straight into the flat gradient buffer (returned grad for ``flat`` is None: the buffer is
-    installed as ``flat.grad`` directly, avoiding an extra 600 MB accumulate pass per step)."""
+# ---- the fused training step as PyTorch custom ops ------------------------------------------------
+# ``ergm::train_step`` (one native forward: loss parts, logits, emotion logits) and
+# ``ergm::train_step_backward`` (the native backward stages: the flat parameter gradient) are
+# registered with torch.library so autograd and torch.compile treat them as opaque operators
+# (register_fake gives their shapes; register_autograd connects them).  The model and its per-shape
+# runner are named by integers (a model handle and the runner's shape key), because custom ops take
+# tensors and plain values only.
+_MODELS: "weakref.WeakValueDictionary[int, GPT2LMHeadModel]" = weakref.WeakValueDictionary()
 
-    @staticmethod
-    def forward(ctx, flat, model, runner, ids, tt, cap_ids, vis, aud, labels, emo_labels):
-        logits, emo, loss = runner.forward(ids, tt, cap_ids, vis, aud, labels, emo_labels, train=True,
-                                           dropout=model._next_dropout())
-        ctx.model, ctx.runner = model, runner
-        ctx.fwd_id = runner.fwd_count
-        ctx.mark_non_differentiable(logits, emo)
-        ctx.set_materialize_grads(False)
-        return loss, logits, emo
 
-    @staticmethod
-    def backward(ctx, grad_loss, grad_logits, grad_emo):
-        if grad_logits is not None or grad_emo is not None:
-            raise NotImplementedError("gradients through logits / emotion_logits are not supported; "
-                                      "back-propagate the loss")
-        model, runner = ctx.model, ctx.runner
-        if runner.fwd_count != ctx.fwd_id:
-            raise RuntimeError("another forward of the same (batch, seq) shape ran after this training forward and "
-                               "overwrote its saved activations: call backward() before the next forward of the "
-                               "shape (e.g. backward per micro-batch for gradient accumulation)")
-        flat = model.flat
-        gl = grad_loss
-        if gl is not None:
-            gl = gl.reshape(-1)[2:3] if gl.numel() == 3 else gl.reshape(1)
-            gl = gl.float().contiguous()
-        if flat.grad is None:
-            post = None
-            opt = model._overlap_opt
-            if opt is not None:
-                post = opt._backward_hook(flat, model)   # per-bucket AdamW, overlapped with backward
-            runner.backward(gl, post)                # writes model.grad_buf
-            flat.grad = model.grad_buf
-        else:
-            # accumulate semantics when the caller did not zero the gradient
-            if flat.grad.data_ptr() == model.grad_buf.data_ptr():
-                tmp = model._grad_tmp()
-                tmp.copy_(model.grad_buf)            # the gradient accumulated so far
-                runner.backward(gl)                  # overwrites grad_buf with this backward's
-                ops.axpy(tmp, model.grad_buf)
-            else:
-                runner.backward(gl)
-                ops.axpy(model.grad_buf, flat.grad)
-        return (None,) * 10
+def _model_of(handle: int) -> "GPT2LMHeadModel":
+    m = _MODELS.get(handle)
+    if m is None:
+        raise RuntimeError(f"ergm: model handle {handle} is gone")
+    return m
+
+
+@torch.library.custom_op("ergm::train_step", mutates_args=())
+def _train_step(flat: torch.Tensor, ids: torch.Tensor, tt: Optional[torch.Tensor], cap_ids: torch.Tensor,
+                vis: Optional[torch.Tensor], aud: Optional[torch.Tensor], labels: Optional[torch.Tensor],
+                emo_labels: Optional[torch.Tensor], handle: int,
+                key: List[int]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    model = _model_of(handle)
+    runner = model._runners[tuple(key)]
+    logits, emo, loss = runner.forward(ids, tt, cap_ids, vis, aud, labels, emo_labels, train=True,
+                                       dropout=model._next_dropout())
+    return loss, logits, emo
+
+
+@_train_step.register_fake
+def _(flat, ids, tt, cap_ids, vis, aud, labels, emo_labels, handle, key):
+    B, S = ids.shape
+    Vp = _model_of(handle).layout.vocab_pad
+    return (flat.new_empty(3), flat.new_empty(B * S, Vp, dtype=torch.bfloat16), flat.new_empty(B, NUM_EMOTIONS))
+
+
+@torch.library.custom_op("ergm::train_step_backward", mutates_args=())
+def _train_step_backward(flat: torch.Tensor, grad_loss: torch.Tensor, handle: int, key: List[int]) -> torch.Tensor:
+    """Gradient of the flat parameter buffer for the runner's last training forward (fresh tensor)."""
+    model = _model_of(handle)
+    model._runners[tuple(key)].backward(grad_loss)
+    return model.grad_buf.clone()
+
+
+@_train_step_backward.register_fake
+def _(flat, grad_loss, handle, key):
+    return torch.empty_like(flat)
+
+
+def _train_step_setup(ctx, inputs, output):
+    handle, key = inputs[8], inputs[9]
+    ctx.handle, ctx.key = handle, key
+    model = _MODELS.get(handle)
+    ctx.fwd_id = model._runners[tuple(key)].fwd_count if model is not None and not _compiling(output[0]) else -1
+    ctx.mark_non_differentiable(output[1], output[2])
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(inputs[0])
+
+
+def _compiling(t: Optional[torch.Tensor] = None) -> bool:
+    """Under torch.compile: Dynamo tracing, or AOTAutograd tracing the backward with fake tensors."""
+    if bool(getattr(torch.compiler, "is_compiling", lambda: False)()):
+        return True
+    if t is not None:
+        from torch._subclasses.fake_tensor import is_fake
+        return bool(is_fake(t))
+    return False
+
+
+def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
+    nones = (None,) * 9
+    if grad_loss is None:
+        return (None,) + nones
+    gl = grad_loss.reshape(-1)[2:3] if grad_loss.numel() == 3 else grad_loss.reshape(1)
+    gl = gl.float().contiguous()
+    if _compiling(grad_loss):  # traced by AOTAutograd: the opaque backward op, its output accumulated by autograd
+        flat, = ctx.saved_tensors
+        return (torch.ops.ergm.train_step_backward(flat, gl, ctx.handle, ctx.key),) + nones
+    model = _model_of(ctx.handle)
+    runner = model._runners[tuple(ctx.key)]
+    if runner.fwd_count != ctx.fwd_id:
+        raise RuntimeError("another forward of the same (batch, seq) shape ran after this training forward and "
+                           "overwrote its saved activations: call backward() before the next forward of the "
+                           "shape (e.g. backward per micro-batch for gradient accumulation)")
+    # eager: the native backward writes straight into the flat gradient buffer, installed as
+    # flat.grad (no 600 MB accumulate pass); the flat input's returned gradient is None
+    flat = model.flat
+    if flat.grad is None:
+        post = None
+        opt = model._overlap_opt
+        if opt is not None:
+            post = opt._backward_hook(flat, model)   # per-bucket AdamW, overlapped with backward
+        runner.backward(gl, post)                    # writes model.grad_buf
+        flat.grad = model.grad_buf
+    elif flat.grad.data_ptr() == model.grad_buf.data_ptr():
+        # accumulate semantics when the caller did not zero the gradient
+        tmp = model._grad_tmp()
+        tmp.copy_(model.grad_buf)                    # the gradient accumulated so far
+        runner.backward(gl)                          # overwrites grad_buf with this backward's
+        ops.axpy(tmp, model.grad_buf)
+    else:
+        runner.backward(gl)
+        ops.axpy(model.grad_buf, flat.grad)
+    return (None,) + nones
+
+
+torch.library.register_autograd("ergm::train_step", _train_step_grad, setup_context=_train_step_setup)
 
 
 class GPT2LMHeadModel(nn.Module):
@@ -146,6 +206,8 @@ class GPT2LMHeadModel(nn.Module):
         self._overlap_opt = None
         self._force_compact_lookup = False  # tests: the data-parallel wte path in one process
         self.process_group = process_group
+        self._handle = id(self)
+        _MODELS[self._handle] = self
         # dropout mask stream: seed from torch's default generator, offset = training forwards so far
         self._drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         self._drop_offset = 0
@@ -237,7 +299,7 @@ class GPT2LMHeadModel(nn.Module):
         return (float(c.attn_pdrop), float(c.resid_pdrop), float(c.embd_pdrop), self._drop_seed, self._drop_offset)
 
     def _runner(self, B, S, vis_rows, has_feat) -> ModelRunner:
-        key = (B, S, vis_rows, has_feat)
+        key = (B, S, vis_rows, int(bool(has_feat)))
         r = self._runners.get(key)
         if r is None:
             r = ModelRunner(self.layout, self.config, self.flat.data, self.flat_b16, self.grad_buf, B, S, vis_rows,
@@ -310,7 +372,8 @@ class GPT2LMHeadModel(nn.Module):
         runner = self._runner(B, S, vis_rows, vis is not None)
         V, Vp = self.config.vocab_size, self.layout.vocab_pad
         if torch.is_grad_enabled() and self.flat.requires_grad and (lab is not None or emo_lab is not None):
-            loss3, logits, emo = _FusedTrainStep.apply(self.flat, self, runner, ids, tt, cap, vis, aud, lab, emo_lab)
+            loss3, logits, emo = torch.ops.ergm.train_step(self.flat, ids, tt, cap, vis, aud, lab, emo_lab, self._handle,
+                                                           list(runner.key))
         else:
             logits, emo, loss3 = runner.forward(ids, tt, cap, vis, aud, lab, emo_lab, train=False)
         out = CausalLMOutputWithEmotionClassification(

@@ -29,6 +29,7 @@ class ModelRunner:
                  B: int, S: int, vis_rows: int, has_features: bool, process_group=None):
         self.layout, self.cfg = layout, cfg
         self.B, self.S = B, S
+        self.key = (B, S, vis_rows, int(bool(has_features)))  # the model's runner key
         self.dev = flat.device
         self.lib = L.load()
         E, Lyr = layout.E, layout.L

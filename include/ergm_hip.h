@@ -89,11 +89,11 @@ typedef enum { ERGM_NK = 0, ERGM_KN = 1 } ergm_b_layout;
 /* Epilogues applied to v = alpha * (A·B)[m][n] (all math fp32):
  *   NONE        C = v
  *   BIAS        C = v + bias[n]
- *   BIAS_GELU   aux_out[m][n] = bf16(v + bias[n]) (pre-activation, for backward);
- *               C = gelu_new(v + bias[n])
+ *   BIAS_GELU   C = gelu_new(v + bias[n]); aux_out[m][n] = bf16(gelu_new'(v + bias[n])) (the
+ *               derivative the backward multiplies by)
  *   BIAS_RESID  C(f32) = aux[m][n](f32) + drop(v + bias[n])      (residual add; aux may == C;
  *               drop = the optional `dropout` site over [M][N], identity when NULL)
- *   GELU_BWD    C = v * gelu_new'(aux[m][n]) with aux = bf16 pre-activation
+ *   GELU_BWD    C = v * aux[m][n] with aux = the bf16 gelu_new' that BIAS_GELU stored
  *   ACCUM       C(f32) = C + v                                   (beta = 1 accumulation)          */
 typedef enum {
     ERGM_EPI_NONE = 0,
@@ -113,9 +113,9 @@ typedef struct {
     int epilogue;   /* ergm_epilogue */
     float alpha;
     const float* bias;   /* [N] f32 or NULL */
-    const void* aux;     /* epilogue input: f32 residual [M][ld_aux] or bf16 pre-activation */
+    const void* aux;     /* epilogue input: f32 residual [M][ld_aux] or bf16 gelu' */
     int ld_aux;
-    void* aux_out;       /* epilogue second output (bf16 pre-activation) [M][ld_aux_out] */
+    void* aux_out;       /* epilogue second output (bf16 gelu' of the pre-activation) [M][ld_aux_out] */
     int ld_aux_out;
     int split_k;         /* 0 = choose automatically, 1 = none, >1 = forced split count */
     const float* alpha_dev;  /* optional device scalar multiplied into alpha (autograd grad_output) */

@@ -94,3 +94,60 @@ def test_dp2_fused_step_matches_single_process(gpu):
     sure = gr.abs() > 10 * (g - gr).abs() + 1e-6
     d = (r["flat"] - r["ref_flat"])[sure].abs().max().item()
     assert d < 1e-5, d
+
+
+def _worker_dropout_trainer(rank, world, port, out_path):
+    """Two ranks (gloo, one GPU) with dropout p = 0.1: masks are indexed by the GLOBAL sample, so the
+    all-reduced gradient equals the single-process gradient of the concatenated batch under the same
+    seed and forward number; the Trainer's epoch metrics are the single-process ones (not 1/world of
+    them)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from ergm_amd.config import ERGMConfig
+    from ergm_amd.model import GPT2LMHeadModel
+    from ergm_amd.optim import FusedAdamW
+    from ergm_amd.train import Trainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = ERGMConfig(vocab_size=500, n_embd=128, n_layer=2, n_head=2, n_positions=64)  # p = 0.1
+    full = [_batch(), _batch()]
+    full[1] = {k: v.roll(1, 0) for k, v in full[1].items()}
+    lo, hi = rank * B // world, (rank + 1) * B // world
+
+    def run(model, batches):
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
+        model._drop_seed = 1234  # the same mask stream in every process
+        st = Trainer(model, opt, process_group=model.process_group).train_epoch(batches)
+        return st, model.flat.grad.clone().cpu(), model.flat.detach().cpu()
+    model = GPT2LMHeadModel(cfg, device=dev, process_group=dist.group.WORLD)
+    model.init_weights(seed=3)
+    st, g, flat = run(model, [{k: v[lo:hi].clone() for k, v in b.items()} for b in full])
+    res = {"loss": st.loss, "ppl": st.ppl, "acc": st.acc, "grad": g, "flat": flat}
+    if rank == 1:
+        torch.save(res, out_path + ".r1")
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        ref = GPT2LMHeadModel(cfg, device=dev)
+        ref.init_weights(seed=3)
+        st, g, flat = run(ref, full)
+        res.update(ref_loss=st.loss, ref_ppl=st.ppl, ref_acc=st.acc, ref_grad=g, ref_flat=flat)
+        torch.save(res, out_path)
+
+
+def test_dp2_dropout_and_trainer_metrics_match_single_process(gpu):
+    torch.cuda.synchronize()
+    path = os.path.join(tempfile.mkdtemp(), "dpd.pt")
+    mp.spawn(_worker_dropout_trainer, args=(2, _free_port(), path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    r1 = torch.load(path + ".r1", weights_only=True)
+    assert torch.equal(r["grad"], r1["grad"]) and torch.equal(r["flat"], r1["flat"])
+    err = ((r["grad"] - r["ref_grad"]).norm() / r["ref_grad"].norm()).item()
+    assert err < 2e-3, err
+    # metrics of two steps (the second after one AdamW update from all-reduced vs single-process
+    # gradients, equal within bf16 rounding): loss rel 1e-3, PPL rel 1e-2, accuracy within one sample
+    assert abs(r["loss"] - r["ref_loss"]) <= 1e-3 * abs(r["ref_loss"]), (r["loss"], r["ref_loss"])
+    assert abs(r["ppl"] - r["ref_ppl"]) <= 1e-2 * r["ref_ppl"], (r["ppl"], r["ref_ppl"])
+    assert abs(r["acc"] - r["ref_acc"]) <= 100.0 / (2 * B) + 1e-9, (r["acc"], r["ref_acc"])

@@ -95,8 +95,11 @@ def test_gemm_f8_epilogues(gpu):
     pre = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     act = torch.empty(M, N + 8, dtype=torch.bfloat16, device=gpu)[:, :N]
     ops.gemm_f8(a8, dev(sa), b8, dev(sb), out=act, epilogue=L.EPI_BIAS_GELU, bias=dev(bias), aux_out=pre)
-    gelu = 0.5 * v * (1 + torch.tanh((2 / torch.pi) ** 0.5 * (v + 0.044715 * v ** 3)))
-    assert (pre.double().cpu() - v).abs().max().item() <= 8e-3 * v.abs().max().item()
+    vv = v.clone().requires_grad_(True)
+    gelu = 0.5 * vv * (1 + torch.tanh((2 / torch.pi) ** 0.5 * (vv + 0.044715 * vv ** 3)))
+    gelu.sum().backward()
+    gelu = gelu.detach()
+    assert (pre.double().cpu() - vv.grad).abs().max().item() <= 8e-3 * vv.grad.abs().max().item()  # gelu'(pre)
     assert (act.double().cpu() - gelu).abs().max().item() <= 8e-3 * gelu.abs().max().item()
     outb = ops.gemm_f8(a8, dev(sa), b8, dev(sb), out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS, bias=dev(bias))
     assert ((outb.double().cpu() - v).norm() / v.norm()).item() < 4e-3

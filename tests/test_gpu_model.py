@@ -360,3 +360,41 @@ def test_second_forward_before_backward_raises(gpu):
     o2 = model(**args)
     with pytest.raises(RuntimeError, match="overwrote"):
         (o1.loss + o2.loss).backward()
+
+
+@pytest.mark.parametrize("B,S", [(4, 64), (3, 32)])
+def test_backward_chains_are_bitwise_the_single_chain(gpu, monkeypatch, B, S):
+    """The backward's data-gradient path split into two concurrent batch-half chains (row-separable
+    kernels on two streams, weight gradients over all tokens) gives bitwise the one-chain gradients
+    (B = 3: unequal halves)."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    res = []
+    for chains in ("1", "2"):
+        monkeypatch.setenv("ERGM_BWD_CHAINS", chains)
+        ocfg, P0, model = _small_model(gpu, S, seed=51)
+        batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=52, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+        out = _run(model, batch, gpu)
+        res.append((out.loss.detach().clone(), model.flat.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_custom_op_registration_and_torch_compile(gpu):
+    """The fused step is the torch.library custom op ergm::train_step (+ its backward op), opaque to
+    autograd and torch.compile: a compiled model gives the eager loss, logits and gradients."""
+    rec = _load("tiny_e64.npz")
+    assert hasattr(torch.ops.ergm, "train_step") and hasattr(torch.ops.ergm, "train_step_backward")
+    outs = []
+    for compiled in (False, True):
+        _, _, _, model, batch = _setup(rec, gpu)
+        kw = {k: v.to(gpu) for k, v in batch.items()}
+        fn = torch.compile(model) if compiled else model
+        model.flat.grad = None
+        out = fn(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                 emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+                 auds=kw["audio_feat"])
+        out.loss.backward()
+        torch.cuda.synchronize()
+        outs.append((out.loss.detach().clone(), out.logits.clone(), model.flat.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

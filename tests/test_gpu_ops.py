@@ -98,25 +98,23 @@ def test_gemm_epilogues(gpu):
     # bias
     out = ops.gemm(A, W, M, N, K, L.MK, L.KN, epilogue=L.EPI_BIAS, bias=bias)
     assert _rel(out, acc + bias.double()) < 1e-5
-    # bias + gelu_new with pre-activation side output
-    pre = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    # bias + gelu_new with the derivative side output
+    dgelu = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     act = ops.gemm(A, W, M, N, K, L.MK, L.KN, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_GELU, bias=bias,
-                   aux_out=pre)
-    z = (acc + bias.double()).float()
+                   aux_out=dgelu)
+    z = (acc + bias.double()).float().requires_grad_(True)
     gelu = 0.5 * z * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (z + 0.044715 * torch.pow(z, 3.0))))
-    assert _rel(pre.float(), z) < 6e-3
-    assert _rel(act.float(), gelu) < 6e-3
+    gelu.sum().backward()
+    assert _rel(act.float(), gelu.detach()) < 6e-3
+    assert _rel(dgelu.float(), z.grad) < 6e-3
     # residual add (in place)
     res = torch.randn(M, N, device=gpu)
     expect = res.double() + acc + bias.double()
     ops.gemm(A, W, M, N, K, L.MK, L.KN, out=res, epilogue=L.EPI_BIAS_RESID, bias=bias, aux=res)
     assert _rel(res, expect) < 1e-6
-    # gelu backward: v * gelu'(pre)
-    x = pre.float().requires_grad_(True)
-    y = 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
-    y.backward(acc.float())
-    out = ops.gemm(A, W, M, N, K, L.MK, L.KN, out_dtype=torch.float32, epilogue=L.EPI_GELU_BWD, aux=pre)
-    assert _rel(out, x.grad) < 1e-5
+    # gelu backward: v * (the stored gelu')
+    out = ops.gemm(A, W, M, N, K, L.MK, L.KN, out_dtype=torch.float32, epilogue=L.EPI_GELU_BWD, aux=dgelu)
+    assert _rel(out, acc * dgelu.double()) < 1e-5
     # accumulate + device alpha
     base = torch.randn(M, N, device=gpu)
     alpha = torch.tensor([0.5], device=gpu)
