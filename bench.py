@@ -339,7 +339,10 @@ def main():
         "optimizer": "FusedAdamW " + (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks})"
                                       if not args.no_overlap_optim else "after backward"),
         "world_size": world,
-        "dp": {"backend": backend, "rehearsal": rehearse} if world > 1 else None,
+        "dp": {"backend": backend, "rehearsal": rehearse, "grad_comm": runner.dp.grad_comm,
+               "grad_bytes_sent_per_rank_per_step": runner.dp.bytes_per_step,
+               "exchange": ("bf16 all-to-all + fp32 chunk sum + bf16 all-gather" if runner.dp.grad_comm == "bf16"
+                            else "fp32 all-reduce")} if world > 1 else None,
         "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
         "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
                           "emotion_acc": round(correct.item() / (B * total), 4)},

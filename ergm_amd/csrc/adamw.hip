@@ -215,3 +215,49 @@ extern "C" int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* 
                        n4, alpha);
     return check_launch("axpy");
 }
+
+// ---- data-parallel gradient exchange in bf16 with fp32 accumulation (ergm_amd/dist.py) ----------
+// Each rank receives one chunk of every rank's bf16 gradient (all-to-all), sums the world copies of its
+// chunk in fp32 in rank order (deterministic, the same sum whichever rank owns it), rounds once to
+// bf16 and all-gathers: half the bytes of an fp32 all-reduce, one rounding of the reduced value.
+namespace ergm {
+__global__ __launch_bounds__(256) void chunk_sum_kernel(const bf16x4* __restrict__ in, int nchunks, size_t chunk4,
+                                                        bf16x4* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < chunk4; i += (size_t)gridDim.x * 256) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < nchunks; ++j) {
+            const bf16x4 v = in[(size_t)j * chunk4 + i];
+            s.x += bf2f(v[0]); s.y += bf2f(v[1]); s.z += bf2f(v[2]); s.w += bf2f(v[3]);
+        }
+        bf16x4 o;
+        o[0] = f2bf(s.x); o[1] = f2bf(s.y); o[2] = f2bf(s.z); o[3] = f2bf(s.w);
+        out[i] = o;
+    }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_kernel(const bf16x4* __restrict__ src, float4* __restrict__ dst,
+                                                       size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        const bf16x4 v = src[i];
+        dst[i] = make_float4(bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3]));
+    }
+}
+}  // namespace ergm
+
+extern "C" int ergm_chunk_sum_bf16(const void* in, int nchunks, size_t chunk, void* out, void* stream) {
+    ERGM_CHECK_ARG(in && out && nchunks > 0 && chunk % 4 == 0, "chunk_sum_bf16: bad argument");
+    const size_t c4 = chunk / 4;
+    if (c4 == 0) return ERGM_OK;
+    hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(c4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
+                       nchunks, c4, (bf16x4*)out);
+    return check_launch("chunk_sum_bf16");
+}
+
+extern "C" int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream) {
+    ERGM_CHECK_ARG(src && dst && n % 4 == 0, "cast_f32: bad argument");
+    const size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    hipLaunchKernelGGL(cast_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)src,
+                       (float4*)dst, n4);
+    return check_launch("cast_f32");
+}

@@ -208,9 +208,7 @@ class ModelRunner:
         ka = Lyr + 1  # ordering-event keys beyond the buckets'
 
         def reduce(a, b):
-            if dp.active:
-                import torch.distributed as dist
-                dist.all_reduce(self.grad[a:b], group=dp.pg, async_op=True).wait()
+            dp.reduce_(self.grad[a:b])
 
         def wte_lm_rows():  # dense LM-head part of g_wte (all rows), then the untouched rows' update
             if compact:
@@ -229,8 +227,7 @@ class ModelRunner:
                 self._ev_count.synchronize()  # recorded right after the forward: long complete
                 n = int(self.row_count_host[0]) * E
                 if dp.active and n:
-                    import torch.distributed as dist
-                    dist.all_reduce(self.compact[:n], group=dp.pg, async_op=True).wait()
+                    dp.reduce_(self.compact[:n])
                 st = torch.cuda.current_stream(self.dev).cuda_stream
                 L.check(lib.ergm_rows_compact(_p(self.row_flags), _p(self.row_pos), Vp, E, _p(self.compact),
                                               C.c_void_p(self.grad.data_ptr() + 4 * wa), 1, C.c_void_p(st)),

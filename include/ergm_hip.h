@@ -267,6 +267,11 @@ int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, 
 int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream);
 /* y[i] += x[i] (f32), used to accumulate gradients across backward calls. */
 int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* stream);
+/* Data-parallel gradient exchange in bf16 with fp32 accumulation (ergm_amd/dist.py): after an
+ * all-to-all of bf16 gradient chunks, out[i] = bf16(Σ_{j < nchunks} in[j·chunk + i]) summed in fp32
+ * in rank order j; after the all-gather, dst[i] = f32(src[i]).  chunk, n multiples of 4.           */
+int ergm_chunk_sum_bf16(const void* in, int nchunks, size_t chunk, void* out, void* stream);
+int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Whole-model executor.  The caller owns every buffer; ergm_model_plan only records pointers and

@@ -43,8 +43,9 @@ def _step(model, opt, batch, dev):
     return g
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, mode="fp32"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["ERGM_DP_GRAD"] = mode
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from ergm_amd.model import GPT2LMHeadModel
@@ -79,16 +80,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_dp2_fused_step_matches_single_process(gpu):
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_dp2_fused_step_matches_single_process(gpu, mode):
+    """Both exchange precisions: "fp32" all-reduce and the default "bf16" all-to-all / fp32 chunk sum /
+    all-gather (ergm_chunk_sum_bf16, ergm_cast_f32 on the GPU)."""
     torch.cuda.synchronize()
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
-    mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), path, mode), nprocs=2, join=True)
     r = torch.load(path, weights_only=True)
     r1 = torch.load(path + ".r1", weights_only=True)
     # both ranks hold the same all-reduced gradient and took the same update
     assert torch.equal(r["grad"], r1["grad"]) and torch.equal(r["flat"], r1["flat"])
     err = ((r["grad"] - r["ref_grad"]).norm() / r["ref_grad"].norm()).item()
-    assert err < 2e-3, err
+    assert err < (2e-3 if mode == "fp32" else 5e-3), err
     # the first AdamW step moves each weight by ±lr·g/(|g|+eps): compare where the sign is unambiguous
     g, gr = r["grad"], r["ref_grad"]
     sure = gr.abs() > 10 * (g - gr).abs() + 1e-6
@@ -103,6 +107,7 @@ def _worker_dropout_trainer(rank, world, port, out_path):
     them)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["ERGM_DP_GRAD"] = "bf16"  # the default exchange
     import torch.distributed as dist
     from ergm_amd.config import ERGMConfig
     from ergm_amd.model import GPT2LMHeadModel
@@ -145,7 +150,9 @@ def test_dp2_dropout_and_trainer_metrics_match_single_process(gpu):
     r1 = torch.load(path + ".r1", weights_only=True)
     assert torch.equal(r["grad"], r1["grad"]) and torch.equal(r["flat"], r1["flat"])
     err = ((r["grad"] - r["ref_grad"]).norm() / r["ref_grad"].norm()).item()
-    assert err < 2e-3, err
+    # the second step's gradient, after one update from bf16-exchanged gradients (two bf16 roundings
+    # per element, ~1.6e-3 rms each step) and a second exchange
+    assert err < 1e-2, err
     # metrics of two steps (the second after one AdamW update from all-reduced vs single-process
     # gradients, equal within bf16 rounding): loss rel 1e-3, PPL rel 1e-2, accuracy within one sample
     assert abs(r["loss"] - r["ref_loss"]) <= 1e-3 * abs(r["ref_loss"]), (r["loss"], r["ref_loss"])
