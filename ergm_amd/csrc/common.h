@@ -29,6 +29,12 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// Diagnostic knock-out switches (ERGM_DIAG_SKIP bitmask; never set in normal runs: the results are wrong):
+// 1 = weight-gradient GEMMs, 2 = LayerNorm dγ/dβ reductions, 4 = AdamW passes, 8 = attention backward,
+// 16 = LayerNorm forward (block LayerNorms), 32 = LayerNorm backward.
+// Used only to measure what a class of launches costs the concurrent step.
+int diag_skip();
+
 // ---- device types -----------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;

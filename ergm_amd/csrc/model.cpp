@@ -156,9 +156,14 @@ struct ergm_model_plan {
     bool drop_on;
     uint64_t* abits;
     int mwords;
-    // kernel probe (bench timing)
+    // kernel probe (bench timing): one event pair (probes 1-4) or a list (probe 5: every weight-gradient
+    // GEMM launch, with its algorithmic FLOPs)
     int probe;
     hipEvent_t ev_begin, ev_end;
+    hipEvent_t* evl_b;
+    hipEvent_t* evl_e;
+    double* evl_flops;
+    int evl_n, evl_k;
     // dry-run sizing
     bool dry;
     size_t need;
@@ -396,11 +401,35 @@ int join_side(ergm_model_plan* P, hipStream_t s, int k) {
     return hipStreamWaitEvent(s, P->ev_join[k], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: stream join");
 }
 
+// Records the probe events around one launch: the single pair when `id` is the active probe, or the
+// next pair of the list when the list probe (5) is active and the launch is a weight-gradient GEMM.
+struct Probe {
+    hipEvent_t end = nullptr;
+    hipStream_t s;
+    Probe(ergm_model_plan* P, int id, hipStream_t s_, double flops = 0.0, bool dw = false) : s(s_) {
+        if (P->dry) return;
+        if (P->probe == id && P->ev_begin) {
+            (void)hipEventRecord(P->ev_begin, s);
+            end = P->ev_end;
+        } else if (P->probe == 5 && dw && P->evl_k < P->evl_n) {
+            const int k = P->evl_k++;
+            (void)hipEventRecord(P->evl_b[k], s);
+            end = P->evl_e[k];
+            if (P->evl_flops) P->evl_flops[k] = flops;
+        }
+    }
+    ~Probe() {
+        if (end) (void)hipEventRecord(end, s);
+    }
+};
+
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB) {
     const int T = P->T;
     ERGM_TRY(fork_side(P, ch));
     hipStream_t s = P->dry ? ch.s[0] : P->side;
+    if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
+    Probe pr(P, 5, s, 2.0 * (M + (P->fused_bias ? 1 : 0)) * N * T, true);
     if (P->fused_bias)
         return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
     ERGM_TRY(gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE));
@@ -441,23 +470,16 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
 
 int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
     if (P->dry || P->ln_pending == 0) return ERGM_OK;
+    if (diag_skip() & 2) {
+        P->ln_pending = 0;
+        return ERGM_OK;
+    }
     ERGM_TRY(fork_side(P, ch));
     const int n = P->ln_pending;
     P->ln_pending = 0;
     return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
 }
 
-struct Probe {  // records the probe events around one launch when `id` is the active probe
-    ergm_model_plan* P;
-    bool on;
-    hipStream_t s;
-    Probe(ergm_model_plan* P_, int id, hipStream_t s_) : P(P_), on(!P_->dry && P_->probe == id && P_->ev_begin), s(s_) {
-        if (on) hipEventRecord(P->ev_begin, s);
-    }
-    ~Probe() {
-        if (on) hipEventRecord(P->ev_end, s);
-    }
-};
 
 inline const float* LF(const ergm_model_plan* P, int l, int t) {
     return P->p.layer_f32 + (int64_t)l * P->p.layer_stride + P->p.layer_off[t];
@@ -619,6 +641,9 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->n_valid = nullptr;
     P->probe = 0;
     P->ev_begin = P->ev_end = nullptr;
+    P->evl_b = P->evl_e = nullptr;
+    P->evl_flops = nullptr;
+    P->evl_n = P->evl_k = 0;
     P->p_attn = P->p_resid = P->p_embd = 0.f;
     P->drop_seed = 0;
     P->drop_offset = 0;
@@ -653,8 +678,23 @@ extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begi
     P->probe = probe;
     P->ev_begin = reinterpret_cast<hipEvent_t>(ev_begin);
     P->ev_end = reinterpret_cast<hipEvent_t>(ev_end);
+    P->evl_n = P->evl_k = 0;
     return ERGM_OK;
 }
+
+extern "C" int ergm_model_set_probe_list(ergm_model_plan* P, void** ev_begin, void** ev_end, double* flops, int n) {
+    ERGM_CHECK_ARG(P && n >= 0 && (n == 0 || (ev_begin && ev_end)), "model_set_probe_list: bad argument");
+    P->probe = n > 0 ? 5 : 0;
+    P->ev_begin = P->ev_end = nullptr;
+    P->evl_b = reinterpret_cast<hipEvent_t*>(ev_begin);
+    P->evl_e = reinterpret_cast<hipEvent_t*>(ev_end);
+    P->evl_flops = flops;
+    P->evl_n = n;
+    P->evl_k = 0;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_probe_count(const ergm_model_plan* P) { return P ? P->evl_k : 0; }
 
 extern "C" int ergm_model_set_dropout(ergm_model_plan* P, float attn_p, float resid_p, float embd_p, uint64_t seed,
                                       uint32_t offset, int batch_base) {
@@ -979,8 +1019,8 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
-        Probe pr(P, 3, ss);
-        ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
+        Probe pr(P, 3, ss, 2.0 * Vp * E * T, true);
+        if (!(diag_skip() & 1)) ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
                       ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, gscale));
         ERGM_TRY(side_mark(P, L + 1));
     }

@@ -336,6 +336,7 @@ using namespace ergm;
 namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
                      int rows, int E, float eps, hipStream_t s, void* yq, int ldq, float* qscale) {
+    if (diag_skip() & 16) return ERGM_OK;
     ERGM_CHECK_ARG(!yq || (qscale && ldq >= E && ldq % 4 == 0), "layernorm_fwd: bad fp8 output");
     auto* q8 = reinterpret_cast<uint8_t*>(yq);
     ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
@@ -390,6 +391,7 @@ int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
                        const DropSite& drop) {
+    if (diag_skip() & 32) return ERGM_OK;
     ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
     const int nb = ln_bwd_nparts(rows);

@@ -1,5 +1,4 @@
-// LDS tile staging shared by the GEMM kernels (gemm.hip) and the fused QKV-projection + attention kernel
-// (attention.hip): bf16 operand tiles of ROWS x 64 (k contiguous) or 64 x ROWS (rows contiguous) with
+// LDS tile staging for the GEMM kernels (gemm.hip): bf16 operand tiles of ROWS x 64 (k contiguous) or 64 x ROWS (rows contiguous) with
 // XOR-swizzled 16-B chunks, filled either through registers (TileLoader) or by LDS-DMA
 // (global_load_lds_dwordx4, GldsTile) with the swizzle applied on the source address, and read as
 // v_mfma_f32_16x16x32_bf16 operand fragments (ds_read_b128, or ds_read_b64_tr_b16 for the transposed

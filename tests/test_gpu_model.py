@@ -217,6 +217,34 @@ def test_inference_and_argument_errors(gpu):
         model(input_ids=kw["input_ids"], caption_ids=kw["caption_ids"], attention_mask=torch.ones(2, 32))
 
 
+def test_executor_entry_points_reject_bad_arguments(gpu):
+    """ERGM_EINVAL -> ValueError through the executor entry points (ergm_model_*): out-of-range
+    layer/stage, bad dropout probabilities, unknown probe, NULL plan; the plan stays usable."""
+    import ctypes as C
+    from ergm_amd import _lib
+    rec = _load("tiny_e64.npz")
+    _, _, _, model, batch = _setup(rec, gpu)
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    model(**kw).loss.backward()
+    runner = next(iter(model._runners.values()))
+    lib, plan = _lib.load(), runner.plan
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bad = [lambda: lib.ergm_model_backward_layer(plan, 999, st),
+           lambda: lib.ergm_model_backward_layer(plan, -1, st),
+           lambda: lib.ergm_model_stage_wait(plan, 10 ** 6, st),
+           lambda: lib.ergm_model_set_dropout(plan, 1.5, 0.1, 0.1, 1, 0, 0),
+           lambda: lib.ergm_model_set_dropout(plan, 0.1, -0.2, 0.1, 1, 0, 0),
+           lambda: lib.ergm_model_set_probe(plan, 99, None, None),
+           lambda: lib.ergm_model_backward_embed(None, st),
+           lambda: lib.ergm_model_forward(None, None, None, None, 0, st)]
+    for i, f in enumerate(bad):
+        with pytest.raises(ValueError):
+            _lib.check(f(), f"case {i}")
+    torch.cuda.synchronize()
+    out = model(**kw)  # still usable after the rejected calls
+    assert abs(out.loss.item() - float(rec["loss"])) < 1e-2
+
+
 def test_iemocap_shape_long_sequence_matches_oracle(gpu):
     """C4's sequence shape (S=512, 20 turns: attention through the tiled kernels, 3·B·S lookups in
     the embedding sort) on a small model, against the live oracle."""

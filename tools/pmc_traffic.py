@@ -69,6 +69,22 @@ def main():
         alg = 2 * T * E + 2 * n0 * E + 2 * T * n0   # A [T,E] + wte [n0,E] bf16 read, logits [T,n0] bf16 written
         res["lm_head_fwd"] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
                               "algorithmic_bytes": alg, "ratio": (fb + wb) / alg}
+    # the weight-gradient GEMM class (bench.py's roofline): every KM x KN pipelined GEMM dispatch; mean
+    # bytes per launch over the class against the mean algorithmic bytes of its C2 launches
+    dwk = [k for k in fetch if "gemm_pipe_kernel<" in k and ", true, true, " in k]
+    if dwk:
+        F, L = 4 * E, cfg.n_layer
+        shapes = [(Vp, E)] + [(F + 1, E), (E + 1, F), (E + 1, E), (E + 1, E), (E + 1, E), (E + 1, 3 * E)] * L + \
+                 [(E + 1, 2 * E * L)]
+        alg = statistics.mean(2 * T * m + 2 * T * n + 4 * m * n for m, n in shapes)
+        nd = sum(len(fetch[k]) for k in dwk)
+        fb = 2.0 * sum(sum(fetch[k]) for k in dwk) / nd
+        wb = sum(sum(write.get(k, [])) for k in dwk) / max(1, sum(len(write.get(k, [])) for k in dwk))
+        res["dw_class"] = {"kernels": [k.split("(")[0] for k in dwk], "dispatches": nd, "fetch_bytes": fb,
+                           "write_bytes": wb, "hbm_bytes": fb + wb, "algorithmic_bytes": alg,
+                           "ratio": (fb + wb) / alg,
+                           "note": "mean per launch over the class; algorithmic = X^T and dY bf16 read once + dW f32 "
+                                   "written once, mean over the step's 74 launches"}
     ad = pick(lambda k: "adamw_kernel" in k)
     if ad:
         k, fb, wb = ad
