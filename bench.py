@@ -415,8 +415,11 @@ def main():
         "world_size": world,
         "dp": {"backend": backend, "rehearsal": rehearse, "grad_comm": runner.dp.grad_comm,
                "grad_bytes_sent_per_rank_per_step": runner.dp.bytes_per_step,
-               "exchange": ("bf16 all-to-all + fp32 chunk sum + bf16 all-gather" if runner.dp.grad_comm == "bf16"
-                            else "fp32 all-reduce")} if world > 1 else None,
+               "exchange": ("bf16 all-to-all + fp32 chunk sum (reduce-scatter), then " +
+                            ("AdamW on this rank's chunk + bf16 all-gather of the updated shadow (ZeRO-1)"
+                             if runner.dp.zero else "bf16 all-gather of the reduced gradient")
+                            if runner.dp.grad_comm == "bf16" else "fp32 all-reduce"),
+               "sharded_optimizer": runner.dp.zero} if world > 1 else None,
         "host_enqueue_ms_per_step": round(1000.0 * t_enq / args.steps, 3),
         "train_metrics": {"mean_loss": round(metrics[0] / total, 4),
                           "emotion_acc": round(metrics[1] / (B * total), 4)},

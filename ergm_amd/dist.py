@@ -18,6 +18,16 @@ data parallelism:
    all-gather of the reduced bf16 chunks, cast back into the fp32 gradient buffer: half the bytes of
    an fp32 all-reduce (2·(N−1)/N · 2 B per parameter), one rounding of the summed gradient, the same
    result on every rank.  "fp32": a plain fp32 all-reduce.  ERGM_DP_GRAD selects (default bf16).
+4. Sharded optimizer (ZeRO-1, bf16 exchange with the overlapped FusedAdamW; ERGM_DP_ZERO=0 disables):
+   the all-to-all + chunk sum above IS a reduce-scatter, so rank r keeps the reduced gradient of its
+   chunk only, applies AdamW to that chunk of the fp32 master, moments and bf16 shadow, and all-gathers
+   the updated bf16 shadow chunks (the forward reads only the shadow).  Same bytes on the wire as the
+   replicated exchange (2 + 2 B per parameter), 1/N of the AdamW pass (30 B/param of HBM traffic) per
+   rank, and the same numbers: the update of every element is computed once, by its owner, from the
+   same bf16-rounded reduced gradient.  Outside a rank's chunks the fp32 master, gradient and moments
+   are stale until ``consolidate_`` all-gathers them (checkpoints, a non-overlapped update).  The tied
+   wte segment keeps the replicated update (its lookup rows are final only after the embedding
+   backward and are exchanged as a compact block).
 
 Works with any torch.distributed backend: "nccl" (= RCCL on ROCm) on GPUs, "gloo" for CPU tests (CPU
 tensors take torch ops for the cast and the chunk sum: that is the host-logic test path; GPU tensors
@@ -44,7 +54,40 @@ class DPSync:
         if self.grad_comm not in ("bf16", "fp32"):
             raise ValueError(f"grad_comm must be 'bf16' or 'fp32' (got {self.grad_comm!r})")
         self._pool = None          # bf16 exchange buffers, reused in stream order by every reduction
+        self._pool32 = None        # fp32 gather buffer (consolidate_)
         self.bytes_per_step = 0    # gradient bytes this rank sent in the last backward (bench report)
+        self.zero = self.grad_comm == "bf16" and os.environ.get("ERGM_DP_ZERO", "1") != "0"
+        # flat ranges [a, b) whose last update ran shard-wise (stale outside this rank's chunk)
+        self.sharded: set = set()
+        self._master = None        # fp32 master whose directly-read elements stay replicated (set_master)
+        self._mranges: List[Tuple[int, int]] = []
+        self._midx: dict = {}
+
+    def set_master(self, master: torch.Tensor, ranges: List[Tuple[int, int]]) -> None:
+        """The fp32 master and the ranges of it the executor reads directly (params.master_read_ranges):
+        after a sharded update their owners' values are broadcast, so the next forward sees the updated
+        LayerNorm parameters, biases, wpe and emotion head on every rank (the shadow covers the rest)."""
+        self._master, self._mranges, self._midx = master, list(ranges), {}
+
+    def _sync_master(self, a: int, b: int, lo: int, hi: int) -> None:
+        import torch.distributed as dist
+        key = (a, b)
+        if key not in self._midx:
+            parts = [torch.arange(max(a, s), min(b, e)) for s, e in self._mranges if s < b and e > a]
+            idx = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.long)
+            own = (idx >= a + lo) & (idx < a + hi)
+            self._midx[key] = (idx.to(self._master.device), own.to(self._master.device))
+        idx, own = self._midx[key]
+        if idx.numel() == 0:
+            return
+        # each element has exactly one owner; the others contribute 0, so the SUM is the owner's value
+        vals = torch.where(own, self._master[idx], torch.zeros((), dtype=self._master.dtype, device=idx.device))
+        self.bytes_per_step += 2 * (self.world - 1) * vals.numel() * 4 // self.world
+        if vals.is_cuda:
+            dist.all_reduce(vals, group=self.pg, async_op=True).wait()
+        else:
+            dist.all_reduce(vals, group=self.pg)
+        self._master[idx] = vals
 
     @property
     def world(self) -> int:
@@ -85,6 +128,59 @@ class DPSync:
         send, recv, gath = self._pool
         return send[:need], recv[:need], gath[:need]
 
+    def chunk(self, n: int) -> int:
+        """Elements per rank of an n-element exchange (a multiple of 8: 16-B aligned chunks)."""
+        W = self.world
+        return -(-(-(-n // W)) // 8) * 8
+
+    def shard(self, n: int) -> Tuple[int, int]:
+        """[lo, hi) of this rank's chunk of an n-element range (may be empty)."""
+        c, r = self.chunk(n), self.rank
+        return min(r * c, n), min((r + 1) * c, n)
+
+    def _exchange(self, t: torch.Tensor):
+        """bf16 all-to-all of t's chunks + the fp32 sum of this rank's chunk over ranks (rounded once to
+        bf16): returns (mine, chunk, gath) with `mine` = this rank's reduced chunk, a view of `gath`."""
+        import torch.distributed as dist
+        W, n = self.world, t.numel()
+        chunk = self.chunk(n)
+        send, recv, gath = self._buffers(chunk, t.device)
+        mine = gath.view(W, chunk)[self.rank]
+        self.bytes_per_step += (W - 1) * chunk * 2
+        if t.is_cuda:
+            from . import _lib as L
+            st = C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+            if W * chunk > n:
+                send[n:].zero_()
+            L.call("ergm_cast_bf16", C.c_void_p(t.data_ptr()), C.c_void_p(send.data_ptr()), n, st)
+            dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+            L.call("ergm_chunk_sum_bf16", C.c_void_p(recv.data_ptr()), W, chunk, C.c_void_p(mine.data_ptr()), st)
+        else:  # gloo on CPU tensors (host-logic tests): the same arithmetic with torch ops
+            send.zero_()
+            send[:n] = t.to(torch.bfloat16)
+            dist.all_to_all_single(recv, send, group=self.pg)
+            mine.copy_(recv.view(W, chunk).float().sum(0).to(torch.bfloat16))
+        return mine, chunk, gath
+
+    def _gather(self, gath: torch.Tensor, mine: torch.Tensor) -> None:
+        import torch.distributed as dist
+        self.bytes_per_step += (self.world - 1) * mine.numel() * mine.element_size()
+        if gath.is_cuda:
+            dist.all_gather_into_tensor(gath, mine, group=self.pg, async_op=True).wait()
+        else:
+            dist.all_gather_into_tensor(gath, mine.clone(), group=self.pg)
+
+    def _cast_f32(self, src: torch.Tensor, dst: torch.Tensor) -> None:
+        n = dst.numel()
+        if n == 0:
+            return
+        if dst.is_cuda:
+            from . import _lib as L
+            L.call("ergm_cast_f32", C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), n,
+                   C.c_void_p(torch.cuda.current_stream(dst.device).cuda_stream))
+        else:
+            dst.copy_(src[:n].float())
+
     def reduce_(self, t: torch.Tensor) -> None:
         """In place on the current stream: t = Σ over ranks of t (SUM), no host synchronisation."""
         if not self.active:
@@ -95,27 +191,64 @@ class DPSync:
             self.bytes_per_step += 2 * (W - 1) * n * t.element_size() // W
             dist.all_reduce(t, group=self.pg, async_op=True).wait()
             return
-        chunk = -(-(-(-n // W)) // 8) * 8
-        send, recv, gath = self._buffers(chunk, t.device)
+        mine, chunk, gath = self._exchange(t)
+        self._gather(gath, mine)
+        self._cast_f32(gath, t)
+
+    def reduce_scatter_(self, t: torch.Tensor) -> Tuple[int, int]:
+        """bf16 exchange without the all-gather: t[lo:hi] (this rank's chunk, returned) = Σ over ranks;
+        the rest of t keeps the local gradient."""
+        mine, chunk, gath = self._exchange(t)
+        lo, hi = self.shard(t.numel())
+        self._cast_f32(mine, t[lo:hi])
+        return lo, hi
+
+    def gather_(self, t: torch.Tensor, lo: int, hi: int) -> None:
+        """All-gather: every rank's chunk [lo_r, hi_r) of t (its shard layout) into t on every rank."""
+        W, n = self.world, t.numel()
+        chunk = self.chunk(n)
+        if t.dtype == torch.bfloat16:
+            gath = self._buffers(chunk, t.device)[2]
+        else:
+            need = W * chunk
+            if self._pool32 is None or self._pool32.numel() < need or self._pool32.device != t.device:
+                self._pool32 = torch.zeros(need, dtype=t.dtype, device=t.device)
+            gath = self._pool32[:need]
         mine = gath.view(W, chunk)[self.rank]
-        self.bytes_per_step += 2 * (W - 1) * chunk * 2
-        if t.is_cuda:
-            from . import _lib as L
-            st = C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
-            if W * chunk > n:
-                send[n:].zero_()
-            L.call("ergm_cast_bf16", C.c_void_p(t.data_ptr()), C.c_void_p(send.data_ptr()), n, st)
-            dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
-            L.call("ergm_chunk_sum_bf16", C.c_void_p(recv.data_ptr()), W, chunk, C.c_void_p(mine.data_ptr()), st)
-            dist.all_gather_into_tensor(gath, mine, group=self.pg, async_op=True).wait()
-            L.call("ergm_cast_f32", C.c_void_p(gath.data_ptr()), C.c_void_p(t.data_ptr()), n, st)
-        else:  # gloo on CPU tensors (host-logic tests): the same arithmetic with torch ops
-            send.zero_()
-            send[:n] = t.to(torch.bfloat16)
-            dist.all_to_all_single(recv, send, group=self.pg)
-            mine.copy_(recv.view(W, chunk).float().sum(0).to(torch.bfloat16))
-            dist.all_gather_into_tensor(gath, mine.clone(), group=self.pg)
-            t.copy_(gath[:n].float())
+        if hi > lo:
+            mine[:hi - lo].copy_(t[lo:hi])
+        self._gather(gath, mine)
+        t.copy_(gath[:n])
+
+    def reduce_then(self, grad: torch.Tensor, a: int, b: int, post=None, shadow: Optional[torch.Tensor] = None) -> None:
+        """Reduce grad[a:b] over ranks, then run the optimizer update ``post(lo, hi)``: shard-wise (ZeRO-1:
+        reduce-scatter, update of this rank's chunk, all-gather of the updated bf16 ``shadow`` chunks)
+        when enabled, otherwise on the whole all-reduced range."""
+        if self.active and self.zero and post is not None and shadow is not None:
+            lo, hi = self.reduce_scatter_(grad[a:b])
+            if hi > lo:
+                post(a + lo, a + hi)
+            self.gather_(shadow[a:b], lo, hi)
+            if self._master is not None:
+                self._sync_master(a, b, lo, hi)
+            self.sharded.add((a, b))
+            return
+        self.reduce_(grad[a:b])
+        if post is not None:
+            post(a, b)
+        self.sharded.discard((a, b))
+
+    def consolidate_(self, tensors, ranges=None) -> None:
+        """All-gather the owners' chunks of every sharded range into each fp32 tensor (master, gradient,
+        moments), on the current stream; collective: every rank calls it."""
+        if not self.active:
+            return
+        for a, b in sorted(self.sharded if ranges is None else ranges):
+            lo, hi = self.shard(b - a)
+            for t in tensors:
+                self.gather_(t[a:b], lo, hi)
+        if ranges is None:
+            self.sharded.clear()
 
     def _side(self, dev):
         if self._stream is None:
@@ -143,19 +276,16 @@ class DPSync:
         with torch.cuda.stream(side):
             fn()
 
-    def bucket_ready(self, k: int, grad: torch.Tensor, post=None, wait=None) -> None:
+    def bucket_ready(self, k: int, grad: torch.Tensor, post=None, wait=None, shadow=None) -> None:
         """Bucket k of the flat gradient buffer `grad` is final on the current stream: start its
-        all-reduce (SUM) on the side stream, then run ``post(a, b)`` there once the reduced values are
-        in place (the overlapped optimizer update of that parameter range)."""
+        reduction (SUM) on the side stream, then run ``post(a, b)`` there once the reduced values are
+        in place (the overlapped optimizer update of that parameter range; shard-wise under ZeRO-1,
+        with the updated ``shadow`` chunks all-gathered)."""
         if not self.active and post is None:
             return
         a, b = self.buckets[k]
-
-        def run():
-            self.reduce_(grad[a:b])  # the side stream waits for the collectives; no host synchronisation
-            if post is not None:
-                post(a, b)
-        self.enqueue(grad, run, k, wait)
+        # the side stream waits for the collectives; no host synchronisation
+        self.enqueue(grad, lambda: self.reduce_then(grad, a, b, post, shadow), k, wait)
 
     def finish(self, grad: torch.Tensor) -> None:
         """Make the current stream wait for every outstanding bucket (no host synchronisation)."""

@@ -266,7 +266,33 @@ class GPT2LMHeadModel(nn.Module):
         if "lm_head.weight" in state_dict and "transformer.wte.weight" not in state_dict:
             self.view("transformer.wte.weight").copy_(state_dict["lm_head.weight"])
         self.refresh_bf16()
+        for r in self._runners.values():  # every rank now holds the full master
+            r.dp.sharded.clear()
         return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    @torch.no_grad()
+    def consolidate_(self) -> None:
+        """Data parallel with the sharded optimizer update (ZeRO-1, ergm_amd/dist.py): all-gather the
+        owners' chunks of the fp32 master, the gradient and the overlapped optimizer's moments, so every
+        rank holds the full values (before a checkpoint, state_dict() or a non-overlapped update).
+        Collective: every rank must call it.  No-op when nothing is sharded."""
+        rs = [r for r in self._runners.values() if r.dp.sharded]
+        if not rs:
+            return
+        ranges = set().union(*(r.dp.sharded for r in rs))
+        ts = [self.flat.data, self.grad_buf]
+        opt = self._overlap_opt
+        st = opt.state.get(self.flat) if opt is not None else None
+        if st:
+            ts += [st["exp_avg"], st["exp_avg_sq"]]
+        rs[0].dp.consolidate_(ts, ranges)
+        for r in rs:
+            r.dp.sharded.clear()
+
+    @property
+    def sharded(self) -> bool:
+        """True while some parameter range is only valid on its owner rank (see consolidate_)."""
+        return any(r.dp.sharded for r in self._runners.values())
 
     @torch.no_grad()
     def refresh_bf16(self) -> None:

@@ -104,6 +104,8 @@ class FusedAdamW(torch.optim.Optimizer):
                     if self.model is not None and p is self.model.flat:
                         self.model._b16_version = p._version
                     continue
+                if self.model is not None and p is self.model.flat and self.model.sharded:
+                    self.model.consolidate_()  # the full update needs every rank's master and moments
                 t = int(st["step"].item())
                 shadow = None
                 if self.model is not None and p is self.model.flat:

@@ -154,3 +154,29 @@ def dp_buckets(layout: Layout) -> List[Tuple[int, int]]:
         b.append(layout.seg[f"layer{i}"])
     b.append(layout.seg["embed"])
     return b
+
+
+# Conv1D weight matrices the executor reads only through the bf16 shadow (ergm_model_params *_b)
+_SHADOW_ONLY = ("attn.c_attn.weight", "attn.c_proj.weight", "crossattention.q_attn.weight",
+                "crossattention.c_proj.weight", "mlp.c_fc.weight", "mlp.c_proj.weight")
+
+
+def master_read_ranges(layout: Layout, fp8: bool = False) -> List[Tuple[int, int]]:
+    """Sorted, merged [start, end) element ranges of the fp32 master that the executor reads directly
+    (LayerNorm parameters, biases, wpe, the emotion head, the tied wte; with fp8 also the caption K/V
+    master, which the weight quantiser reads): everything except the Conv1D weight matrices, which it
+    reads through the bf16 shadow.  The sharded optimizer update (dist.py, ZeRO-1) keeps these
+    replicated in fp32 on every rank."""
+    skip = {f"transformer.h.{i}.{t}" for i in range(layout.L) for t in _SHADOW_ONLY}
+    skip |= {"transformer.visual_proj.weight", "transformer.audio_proj.weight", "transformer.wte.weight"}
+    skip |= {f"transformer.h.{i}.crossattention.c_attn.{t}" for i in range(layout.L) for t in ("weight", "bias")}
+    if not fp8:
+        skip.add("__capkv_w")
+    iv = sorted((v.offset, v.offset + v.numel) for k, v in layout.views.items() if k not in skip)
+    out: List[Tuple[int, int]] = []
+    for a, b in iv:
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib as L
 from .dist import DPSync
-from .params import Layout, dp_buckets
+from .params import Layout, dp_buckets, master_read_ranges
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -86,7 +86,9 @@ class ModelRunner:
         self.per_stage_join = os.environ.get("ERGM_SIDE_JOINS", "0") == "1"
         L.check(self.lib.ergm_model_set_side_joins(self.plan, int(self.per_stage_join)), "ergm_model_set_side_joins")
         self.grad = grad
+        self.shadow = flat_b16
         self.dp = DPSync(process_group, dp_buckets(layout))
+        self.dp.set_master(flat, master_read_ranges(layout, bool(getattr(cfg, "fp8", False))))
         self.n_valid = torch.zeros(4, dtype=torch.int32, device=self.dev)  # [LM, emotion] valid-label counts
         self._inputs = None
         # every forward overwrites the activations saved for backward: the autograd bridge checks that
@@ -218,8 +220,8 @@ class ModelRunner:
 
         def capwpe():
             if compact:
-                reduce(ca, cb)
-            if post is not None:
+                dp.reduce_then(self.grad, ca, cb, post, self.shadow)
+            elif post is not None:
                 post(ca, cb)
 
         def wte_lookup_rows():  # lookup part of the touched rows, then their update
@@ -243,14 +245,14 @@ class ModelRunner:
         for i, l in enumerate(reversed(range(Lyr))):
             L.check(lib.ergm_model_backward_layer(self.plan, l, s), "ergm_model_backward_layer")
             if i >= 1:
-                dp.bucket_ready(i - 1, self.grad, post, wait=stage(l + 1))
+                dp.bucket_ready(i - 1, self.grad, post, wait=stage(l + 1), shadow=self.shadow)
             if split_wte and i == 1:
                 dp.enqueue(self.grad, wte_lm_rows, ka, wait=stage(Lyr + 1))
         if compact:
             self._ev_zero.wait(s.value)  # compact rows zeroed before the lookup sums land in them
             self._compact_ready = False
         L.check(lib.ergm_model_backward_embed(self.plan, s), "ergm_model_backward_embed")
-        dp.bucket_ready(Lyr - 1, self.grad, post)
+        dp.bucket_ready(Lyr - 1, self.grad, post, shadow=self.shadow)
         if split_wte:
             if Lyr == 1:
                 dp.enqueue(self.grad, wte_lm_rows, ka)

@@ -111,6 +111,8 @@ class Trainer:
             va = self.validation(valid_loader)
             if va.ppl < self.best_ppl:
                 self.best_ppl = va.ppl
+                if self.ckpt_dir is not None and hasattr(self.model, "consolidate_"):
+                    self.model.consolidate_()  # collective: every rank (the sharded optimizer update)
                 if self.ckpt_dir is not None and self._rank0():
                     path = os.path.join(self.ckpt_dir, f"best_ckpt_epoch={epoch}_valid_ppl={self.best_ppl:.4f}.ckpt")
                     self.save(path)

@@ -119,3 +119,51 @@ def test_dp2_matches_single_process_gradient(mode):
 def test_grad_comm_mode_validated():
     with pytest.raises(ValueError):
         DPSync(None, [], grad_comm="fp16")
+
+
+def _zero_worker(rank, world, port, out_path):
+    """The sharded update (ZeRO-1) against the replicated one, same gradients: a plain SGD-like
+    ``post`` stands in for the optimizer; after consolidate_ the master, the gradient and the bf16
+    shadow must be bitwise those of the replicated bf16 exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    n = 4 * 1000 + 64
+    buckets = [(0, 1000), (1000, 2000), (2000, 4064)]
+    res = {}
+    for zero in (False, True):
+        g = torch.randn(n, generator=torch.Generator().manual_seed(7 + rank))
+        p = torch.randn(n, generator=torch.Generator().manual_seed(1))
+        shadow = p.to(torch.bfloat16)
+        dp = DPSync(dist.group.WORLD, buckets, grad_comm="bf16")
+        dp.zero = zero
+        dp.set_master(p, [(10, 30), (990, 1010), (3000, 3100)])  # "directly read" fp32 ranges
+
+        def post(a, b):
+            p[a:b] -= 0.1 * g[a:b]
+            shadow[a:b] = p[a:b].to(torch.bfloat16)
+        dp.begin()
+        for k in range(len(buckets)):
+            dp.bucket_ready(k, g, post, shadow=shadow)
+        dp.finish(g)
+        sharded = set(dp.sharded)
+        # before consolidation the directly-read master ranges are already replicated and current
+        pre = torch.cat([p[10:30], p[990:1010], p[3000:3100]]).clone()
+        dp.consolidate_([p, g])
+        post_ = torch.cat([p[10:30], p[990:1010], p[3000:3100]])
+        res[zero] = (p.clone(), g.clone(), shadow.clone(), sharded, dp.bytes_per_step, torch.equal(pre, post_))
+    ok = all(torch.equal(res[True][i], res[False][i]) for i in range(3)) and res[True][5]
+    if rank == 0:
+        torch.save({"ok": ok, "sharded": sorted(res[True][3]), "none": sorted(res[False][3])}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero1_sharded_update_matches_replicated():
+    path = os.path.join(tempfile.mkdtemp(), "z.pt")
+    mp.spawn(_zero_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    assert r["ok"]
+    assert r["sharded"] == [(0, 1000), (1000, 2000), (2000, 4064)] and r["none"] == []

@@ -45,7 +45,8 @@ def _step(model, opt, batch, dev):
 
 def _worker(rank, world, port, out_path, mode="fp32"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["ERGM_DP_GRAD"] = mode
+    os.environ["ERGM_DP_GRAD"] = "fp32" if mode == "fp32" else "bf16"
+    os.environ["ERGM_DP_ZERO"] = "1" if mode == "bf16" else "0"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from ergm_amd.model import GPT2LMHeadModel
@@ -60,7 +61,12 @@ def _worker(rank, world, port, out_path, mode="fp32"):
     model.init_weights(seed=3)
     opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
     g = _step(model, opt, local, dev)
-    res = {"grad": g.cpu(), "flat": model.flat.detach().cpu()}
+    res = {"sharded": model.sharded}
+    model.consolidate_()  # sharded update (ZeRO-1): gather master, gradient and moments
+    torch.cuda.synchronize()
+    st = opt.state[model.flat]
+    res.update(grad=model.flat.grad.clone().cpu(), flat=model.flat.detach().cpu(), m=st["exp_avg"].cpu(),
+               v=st["exp_avg_sq"].cpu(), shadow=model.flat_b16.cpu())
     if rank == 1:
         torch.save(res, out_path + ".r1")
     dist.barrier()
@@ -80,15 +86,27 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16"])
-def test_dp2_fused_step_matches_single_process(gpu, mode):
-    """Both exchange precisions: "fp32" all-reduce and the default "bf16" all-to-all / fp32 chunk sum /
-    all-gather (ergm_chunk_sum_bf16, ergm_cast_f32 on the GPU)."""
-    torch.cuda.synchronize()
+def _run(mode):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     mp.spawn(_worker, args=(2, _free_port(), path, mode), nprocs=2, join=True)
-    r = torch.load(path, weights_only=True)
-    r1 = torch.load(path + ".r1", weights_only=True)
+    return torch.load(path, weights_only=True), torch.load(path + ".r1", weights_only=True)
+
+
+_RUNS = {}
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16nz", "bf16"])
+def test_dp2_fused_step_matches_single_process(gpu, mode):
+    """Exchange precisions: "fp32" all-reduce; "bf16nz" the bf16 all-to-all / fp32 chunk sum /
+    all-gather (ergm_chunk_sum_bf16, ergm_cast_f32) with the replicated update; "bf16" (the default) the
+    same exchange with the sharded update (ZeRO-1) — bitwise the replicated one after consolidate_."""
+    torch.cuda.synchronize()
+    r, r1 = _RUNS[mode] = _run(mode)
+    assert r["sharded"] == (mode == "bf16") and r1["sharded"] == (mode == "bf16")
+    if mode == "bf16" and "bf16nz" in _RUNS:
+        z = _RUNS["bf16nz"][0]
+        for k in ("grad", "flat", "m", "v", "shadow"):
+            assert torch.equal(r[k], z[k]), k
     # both ranks hold the same all-reduced gradient and took the same update
     assert torch.equal(r["grad"], r1["grad"]) and torch.equal(r["flat"], r1["flat"])
     err = ((r["grad"] - r["ref_grad"]).norm() / r["ref_grad"].norm()).item()
@@ -125,6 +143,7 @@ def _worker_dropout_trainer(rank, world, port, out_path):
         opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
         model._drop_seed = 1234  # the same mask stream in every process
         st = Trainer(model, opt, process_group=model.process_group).train_epoch(batches)
+        model.consolidate_()
         return st, model.flat.grad.clone().cpu(), model.flat.detach().cpu()
     model = GPT2LMHeadModel(cfg, device=dev, process_group=dist.group.WORLD)
     model.init_weights(seed=3)
