@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 3  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 4  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -37,7 +37,7 @@ class GemmDesc(C.Structure):
                 ("ldc", C.c_int), ("a_layout", C.c_int), ("b_layout", C.c_int), ("c_dtype", C.c_int),
                 ("epilogue", C.c_int), ("alpha", C.c_float), ("bias", C.c_void_p), ("aux", C.c_void_p),
                 ("ld_aux", C.c_int), ("aux_out", C.c_void_p), ("ld_aux_out", C.c_int), ("split_k", C.c_int),
-                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout))]
+                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p)]
 
 
 class ModelDims(C.Structure):

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "common.h"
 #include "tiles.h"
@@ -43,6 +44,8 @@ struct GemmArgs {
     const float* b_scale;  // fp8 GEMM: per-column dequantisation scale of B [N]
     int nt_store;          // C written with non-temporal stores (streamed output)
     DropSite drop;         // BIAS_RESID: dropout of the residual branch (src/model.py:245,266), rows m, cols n
+    float* colsum;         // KM x KN, EPI_NONE: bias gradient alpha·Σ_k B[k][n] -> colsum[n] (nullptr: none)
+    float* colsum_part;    // split-K: per-split partial column sums [z][N] (combined by splitk_reduce_kernel)
 };
 
 template <int EPI, bool OUT_BF16>
@@ -357,34 +360,81 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
 
     FragReader<BM, A_KM> la;
     FragReader<BN, B_KN> lb;
-    for (int kt = 0; kt < nk; ++kt) {
-        // stages this wave issued after kt: min(NS-2, nk-1-kt); wait until stage kt has landed
-        const int after = min(NS - 2, nk - 1 - kt);
-        wait_stages<LPS, NS - 2>(after);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot to refill are done
-        __builtin_amdgcn_s_barrier();
-        if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
-        const char* st = smem + (kt % NS) * STAGE;
+    // weight-gradient bias: the waves of the last tile row with wm == 0 also sum the B (dY) fragments they
+    // read: lane l holds B[k = 8(l>>4) .. +7][n = l & 15] of each 16-column fragment
+    constexpr bool CS = A_KM && B_KN && EPI == ERGM_EPI_NONE && !OUT_BF16;
+    const bool do_cs = CS && a.colsum && tm == a.tiles_m - 1 && wm == 0;
+    float cs[FN];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            bf16x8 fa[FM], fb[FN];
+    for (int j = 0; j < FN; ++j) cs[j] = 0.f;
+    // two copies of the main loop: only the summing waves carry the dot products (a runtime flag inside
+    // one loop made the compiler unswitch it and raised the register count for every tile)
+    auto main_loop = [&](auto sum_tag) {
+        constexpr bool SUM = decltype(sum_tag)::value;
+        for (int kt = 0; kt < nk; ++kt) {
+            // stages this wave issued after kt: min(NS-2, nk-1-kt); wait until stage kt has landed
+            const int after = min(NS - 2, nk - 1 - kt);
+            wait_stages<LPS, NS - 2>(after);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot to refill are done
+            __builtin_amdgcn_s_barrier();
+            if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+            const char* st = smem + (kt % NS) * STAGE;
 #pragma unroll
-            for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fa[FM], fb[FN];
 #pragma unroll
-            for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+                for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+                for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+                if constexpr (SUM) {  // packed bf16 dot products against ones: 4 v_dot2 per fragment
+                    const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    if constexpr (DIRECT)  // Cᵀ fragments (store_tile_direct)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-                    else
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < FN; ++j) {
+                        float t = cs[j];
+                        t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(fb[j], fb[j], 0, 1), one, t, false);
+                        t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(fb[j], fb[j], 2, 3), one, t, false);
+                        t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(fb[j], fb[j], 4, 5), one, t, false);
+                        t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(fb[j], fb[j], 6, 7), one, t, false);
+                        cs[j] = t;
+                    }
                 }
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        if constexpr (DIRECT)  // Cᵀ fragments (store_tile_direct)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+                        else
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    }
+            }
         }
+    };
+    if constexpr (CS) {
+        if (do_cs) main_loop(std::true_type{});
+        else main_loop(std::false_type{});
+    } else {
+        main_loop(std::false_type{});
     }
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
+    if constexpr (CS) {
+        if (do_cs) {  // sum the four 16-lane rows (k groups), lane position (column) preserved
+            const int lane = threadIdx.x & 63;
+            float* dst = a.slab ? a.colsum_part + (size_t)blockIdx.z * a.N : a.colsum;
+            const float sc = a.slab ? 1.0f : alpha;  // split-K: the reduce kernel applies alpha
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                float v = cs[j];
+                auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                const int n = n0 + wn * WN + j * 16 + lane;
+                if (lane < 16 && n < a.N) dst[n] = sc * v;
+            }
+        }
+    }
     if constexpr (DIRECT) {
         store_tile_direct<WGN, EPI, OUT_BF16, FM, FN, WM, WN>(a, acc, m0, n0, alpha);
     } else {
@@ -572,6 +622,32 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int spli
         int m = (int)(i / a.N), n = (int)(i % a.N);
         epilogue_store<EPI, OUT_BF16>(a, m, n, alpha * s);
     }
+    if (a.colsum && a.colsum_part) {  // the weight-gradient bias: per-split column sums, in z order
+        for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < a.N; n += gridDim.x * blockDim.x) {
+            float s = 0.f;
+            for (int z = 0; z < splits; ++z) s += a.colsum_part[(size_t)z * a.N + n];
+            a.colsum[n] = alpha * s;
+        }
+    }
+}
+
+// Bias gradient for the kernels without the in-GEMM column sum (register-staged / warp-specialised
+// configurations): out[n] = alpha·Σ_k B[k][n], B = [K][ldb] bf16; 4 row groups per column, fixed-order
+// combine (deterministic).
+__global__ __launch_bounds__(256) void colsum_kn_kernel(const __bf16* __restrict__ B, int K, int N, int ldb,
+                                                        float alpha, const float* alpha_dev, float* __restrict__ out) {
+    __shared__ float part[4][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int n = blockIdx.x * 64 + c;
+    float s = 0.f;
+    if (n < N)
+        for (int k = g; k < K; k += 4) s += bf2f(B[(size_t)k * ldb + n]);
+    part[g][c] = s;
+    __syncthreads();
+    if (g == 0 && n < N) {
+        const float al = alpha_dev ? alpha * *alpha_dev : alpha;
+        out[n] = al * (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -655,12 +731,12 @@ static std::mutex g_over_mu;
 // automatic choice; profiles/r01_step_tune_*.json).  Runtime overrides take precedence.
 static constexpr GemmOverride kStepTuned[] = {
     // config 2 (GPT-2-small, B=16, S=128; forward GEMMs run per batch half, M = 1024)
-    {3073, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient
-    {769, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient
+    {3072, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient
+    {768, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient
     {1024, 2304, 768, ERGM_MK, ERGM_KN, 3, 1},   // c_attn forward
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
     {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
-    {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+    {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
     {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
     {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
 };
@@ -991,7 +1067,7 @@ extern "C" size_t ergm_gemm_workspace_size(const ergm_gemm_desc* d) {
     if (!d) return 0;
     GemmPlan p = plan_gemm(d);
     if (p.split <= 1) return 0;
-    return (size_t)p.split * d->M * d->N * sizeof(float);
+    return (size_t)p.split * d->M * d->N * sizeof(float) + (d->bias_grad ? (size_t)p.split * d->N * sizeof(float) : 0);
 }
 
 extern "C" int ergm_gemm_set_override(int M, int N, int K, int a_layout, int b_layout, int cfg, int split) {
@@ -1055,6 +1131,9 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     ERGM_TRY(check_dropout(d->dropout));
     ERGM_CHECK_ARG(!d->dropout || d->dropout->p == 0.f || e == ERGM_EPI_BIAS_RESID,
                    "ergm_gemm: dropout applies to the BIAS_RESID epilogue only");
+    ERGM_CHECK_ARG(!d->bias_grad || (d->a_layout == ERGM_KM && d->b_layout == ERGM_KN && e == ERGM_EPI_NONE &&
+                                     d->c_dtype == ERGM_F32),
+                   "ergm_gemm: bias_grad needs a_layout KM, b_layout KN, epilogue NONE and f32 C");
 
     trace_shape(d);
     GemmPlan p = plan_gemm(d);
@@ -1083,11 +1162,16 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     a.nt_store = nt_env && ((d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
                             (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE));
     hipStream_t s = as_stream(stream);
+    // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
+    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0;
+    a.colsum = cs_in ? d->bias_grad : nullptr;
+    a.colsum_part = nullptr;
     if (p.split > 1) {
-        size_t need = (size_t)p.split * d->M * d->N * sizeof(float);
+        size_t need = (size_t)p.split * d->M * d->N * sizeof(float) + (d->bias_grad ? (size_t)p.split * d->N * 4 : 0);
         ERGM_CHECK_ARG(ws && ws_bytes >= need, "ergm_gemm: split-K %d needs %zu workspace bytes (got %zu)", p.split,
                        need, ws_bytes);
         a.slab = reinterpret_cast<float*>(ws);
+        if (cs_in) a.colsum_part = a.slab + (size_t)p.split * d->M * d->N;
     }
     const bool ob = d->c_dtype == ERGM_BF16;
 #define ERGM_EPI_CASE(E)                                                  \
@@ -1108,5 +1192,8 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
         ERGM_EPI_CASE(ERGM_EPI_ACCUM)
     }
 #undef ERGM_EPI_CASE
+    if (d->bias_grad && !cs_in)
+        hipLaunchKernelGGL(colsum_kn_kernel, dim3(cdiv(d->N, 64)), dim3(256), 0, s, a.B, d->K, d->N, d->ldb, d->alpha,
+                           d->alpha_dev, d->bias_grad);
     return check_launch("ergm_gemm");
 }

@@ -29,7 +29,6 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
 int quant_weights_fp8(const WqJobs& J, hipStream_t s);
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
                    hipStream_t s);
-int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
@@ -73,7 +72,6 @@ struct ergm_model_plan {
     // Activations that feed a weight-gradient GEMM carry a constant ones column (index E or F) so the
     // dW GEMM over K+1 rows also yields the bias gradient (each bias is stored right after its weight).
     int XE, XF;
-    bool fused_bias;
     // activations
     float** resid;  // 3L+1 residual-stream tensors [T][E] f32
     std::vector<float*> resid_v;
@@ -313,13 +311,13 @@ uint64_t* attn_bits(const ergm_model_plan* P, int l, int cross, int b0) {
 int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, int lda, int al, const void* B,
          int ldb, int bl, void* C, int ldc, int cdt, int epi, const float* bias = nullptr, const void* aux = nullptr,
          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const float* alpha_dev = nullptr,
-         const ergm_dropout* dropout = nullptr) {
+         const ergm_dropout* dropout = nullptr, float* bias_grad = nullptr) {
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
     g.a_layout = al; g.b_layout = bl; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
-    g.split_k = 0; g.alpha_dev = alpha_dev; g.dropout = dropout;
+    g.split_k = 0; g.alpha_dev = alpha_dev; g.dropout = dropout; g.bias_grad = bias_grad;
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
@@ -341,16 +339,7 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
     return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
 }
 
-int colsum(ergm_model_plan* P, hipStream_t s, const void* X, int dt, int rows, int cols, int ldx, float* out) {
-    ERGM_TRY(ws_need(P, ergm_colsum_workspace_size(rows, cols)));
-    if (P->dry) return ERGM_OK;
-    char* ws = (s != nullptr && s == P->side) ? P->scratch2 : (s != nullptr && s == P->fwd2) ? P->scratch3 : P->scratch;
-    return ergm_colsum(X, dt, rows, cols, ldx, out, 0, ws, P->scratch_bytes, s);
-}
 
-// Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]).
-// With fused_bias the A operand's column M is all ones and gB == gW + M·N, so one GEMM over M+1
-// rows writes [gW; gB]; otherwise the bias gradient is a separate column sum of dY.
 // Fork/join events order two streams of the same device: device-scope release is enough, and skipping
 // the system-scope fence avoids an L2 writeback at every record on the critical stream.
 constexpr unsigned kSyncEv = hipEventDisableTiming | hipEventDisableSystemFence;
@@ -423,17 +412,17 @@ struct Probe {
     }
 };
 
+// Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]) and its
+// bias gradient gB[N] = Σ_t dY[t][n], summed by the same GEMM from the dY fragments it stages.
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB) {
     const int T = P->T;
     ERGM_TRY(fork_side(P, ch));
     hipStream_t s = P->dry ? ch.s[0] : P->side;
     if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
-    Probe pr(P, 5, s, 2.0 * (M + (P->fused_bias ? 1 : 0)) * N * T, true);
-    if (P->fused_bias)
-        return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
-    ERGM_TRY(gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE));
-    return colsum(P, s, dY, ERGM_BF16, T, N, ldy, gB);
+    Probe pr(P, 5, s, 2.0 * M * N * T + (double)N * T, true);
+    return gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE, nullptr, nullptr, 0,
+                nullptr, 0, nullptr, nullptr, gB);
 }
 
 // LayerNorm backward on the critical chain(s): rows [r0, r0 + rows) of the residual stream; its dγ/dβ
@@ -528,9 +517,7 @@ extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     P.L2E = 2 * dims->n_embd * dims->n_layer;
     size_t act = carve(&P, nullptr);
     P.dry = true;
-    P.fused_bias = false;  // the colsum fallback needs the larger scratch
     P.need = ergm_embed_bwd_workspace_size(P.T);
-    P.need = std::max(P.need, ergm_colsum_workspace_size(P.T, std::max(P.L2E, dims->n_inner)));
     P.labels = P.emo_labels = nullptr;
     P.fwd2 = nullptr;
     for (int chains = 1; chains <= 2; ++chains) {  // size for the whole batch and for its halves
@@ -608,31 +595,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->need = 0;
     P->have_fwd = false;
     P->ln_pending = 0;
-    // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py
-    // lays the flat buffers out that way); otherwise fall back to separate column sums.
-    {
-        const int64_t E = d.n_embd, F = d.n_inner;
-        const int64_t* o = P->p.layer_off;
-        auto follows = [&](int w, int b, int64_t K, int64_t N) { return o[b] == o[w] + K * N; };
-        P->fused_bias = follows(ERGM_T_ATTN_W, ERGM_T_ATTN_B, E, 3 * E) && follows(ERGM_T_APROJ_W, ERGM_T_APROJ_B, E, E) &&
-                        follows(ERGM_T_XQ_W, ERGM_T_XQ_B, E, E) && follows(ERGM_T_XPROJ_W, ERGM_T_XPROJ_B, E, E) &&
-                        follows(ERGM_T_FC_W, ERGM_T_FC_B, E, F) && follows(ERGM_T_MPROJ_W, ERGM_T_MPROJ_B, F, E) &&
-                        P->p.g_capkv_b == P->p.g_capkv_w + E * P->L2E;
-        // the ones columns are never overwritten by the producers (they write columns < E / < F)
-        int rc = ERGM_OK;
-        for (int l = 0; l < d.n_layer && rc == ERGM_OK; ++l) {
-            LayerActs& a = P->la[l];
-            const void* cols[5] = {a.ln1, a.lnx, a.ln2, a.ao, a.xo};
-            for (int i = 0; i < 5 && rc == ERGM_OK; ++i) rc = fill_ones_col((void*)cols[i], P->T, P->XE, d.n_embd, nullptr);
-            if (rc == ERGM_OK) rc = fill_ones_col(a.act, P->T, P->XF, d.n_inner, nullptr);
-        }
-        if (rc == ERGM_OK) rc = fill_ones_col(P->cap, P->T, P->XE, d.n_embd, nullptr);
-        if (rc == ERGM_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = fail(ERGM_EHIP, "model_create: sync");
-        if (rc != ERGM_OK) {
-            ergm_model_destroy(P);
-            return rc;
-        }
-    }
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
     P->row_flag = nullptr;

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 3
+#define ERGM_ABI_VERSION 4
 
 typedef enum {
     ERGM_OK = 0,
@@ -120,6 +120,10 @@ typedef struct {
     int split_k;         /* 0 = choose automatically, 1 = none, >1 = forced split count */
     const float* alpha_dev;  /* optional device scalar multiplied into alpha (autograd grad_output) */
     const ergm_dropout* dropout;  /* BIAS_RESID only: residual-branch dropout (rows m, cols n); NULL = none */
+    float* bias_grad;    /* a_layout KM + b_layout KN (a weight gradient Xᵀ·dY), epilogue NONE, f32 C only:
+                          * also write alpha·Σ_k B[k][n] (the Conv1D bias gradient, column sums of dY over
+                          * the K tokens) to bias_grad[n], f32 [N]; NULL = none.  Computed from the B
+                          * fragments the GEMM already stages (no second pass over dY), deterministic. */
 } ergm_gemm_desc;
 
 /* Tuning hook (calling thread only): force pipelined-kernel configuration `cfg` (tile / wave grid /
