@@ -312,7 +312,7 @@ def main():
     if args.probe == 5:
         tp = time.perf_counter()
         for pb in plist:
-            _lib.check(lib.ergm_model_set_probe_list(runner.plan, pb[2], pb[3], pb[4], NPR), "ergm_model_set_probe_list")
+            _lib.check(lib.ergm_model_set_probe_list(runner.plan, 5, pb[2], pb[3], pb[4], NPR), "ergm_model_set_probe_list")
             step()
             counts.append(lib.ergm_model_probe_count(runner.plan))
         lib.ergm_model_set_probe(runner.plan, 0, None, None)
@@ -323,6 +323,22 @@ def main():
         for (b, e, _, _, fl), n in zip(plist, counts):
             durs += [b[k].elapsed_ms(e[k]) for k in range(n)]
             flops += [fl[k] for k in range(n)]
+        if os.environ.get("ERGM_BENCH_FWD_DETAIL"):  # the same for the block forward GEMMs (list probe 6)
+            NF = 6 * 2 * cfg.n_layer + 8
+            fl = []
+            for _ in range(3):
+                b, e = [_lib.HipEvent() for _ in range(NF)], [_lib.HipEvent() for _ in range(NF)]
+                arr = ((C.c_void_p * NF)(*[x.ev.value for x in b]), (C.c_void_p * NF)(*[x.ev.value for x in e]),
+                       (C.c_double * NF)())
+                _lib.check(lib.ergm_model_set_probe_list(runner.plan, 6, arr[0], arr[1], arr[2], NF), "probe list")
+                step()
+                fl.append((b, e, arr[2], lib.ergm_model_probe_count(runner.plan)))
+            lib.ergm_model_set_probe(runner.plan, 0, None, None)
+            n = min(x[3] for x in fl)
+            det = [{"k": k, "gflop": fl[0][2][k] / 1e9,
+                    "us": 1000.0 * sum(x[0][k].elapsed_ms(x[1][k]) for x in fl) / len(fl)} for k in range(n)]
+            with open(os.environ["ERGM_BENCH_FWD_DETAIL"], "w") as f:
+                json.dump(det, f, indent=0)
         if os.environ.get("ERGM_BENCH_DW_DETAIL"):  # per launch position: mean in-step duration and FLOPs
             n = min(counts)
             det = [{"k": k, "gflop": plist[0][4][k] / 1e9,

@@ -101,7 +101,7 @@ _SIGS = {
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),
     "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
-    "ergm_model_set_probe_list": (i32, [vp, vp, vp, vp, i32]),
+    "ergm_model_set_probe_list": (i32, [vp, i32, vp, vp, vp, i32]),
     "ergm_model_probe_count": (i32, [vp]),
     "ergm_model_set_row_flags": (i32, [vp, vp, i32]),
     "ergm_model_set_lookup_compact": (i32, [vp, vp, vp]),

