@@ -173,9 +173,9 @@ def main():
                          "1 = LM-head forward main launch, 2 = LM-head dX, 3 = LM-head dW, 4 = caption K/V GEMM")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
-    ap.add_argument("--gpu-only", action="store_true",
-                    help="diagnostic: also time K steps enqueued behind a spin kernel (no host in the loop) and "
-                         "report gpu_only_ms_per_step")
+    ap.add_argument("--no-gpu-only", dest="gpu_only", action="store_false",
+                    help="skip the extra K steps enqueued behind a spin kernel (no host in the loop) that give "
+                         "gpu_only_ms_per_step")
     ap.add_argument("--pdrop", type=float, default=None,
                     help="attn/resid/embd dropout (default: the config's 0.1, as the reference trains; 0 = off)")
     args = ap.parse_args()
@@ -378,7 +378,7 @@ def main():
         probe_flops = sum(flops) / len(flops)
         achieved = sum(flops) / (sum(durs) * 1e-3) / 1e12
         probe_name = (f"weight-gradient GEMM class (dW = X^T.dY, KM x KN operands, fp32 out; the step's largest "
-                      f"time class): {n_l} launches per step = every block's 6 Conv1D dW (bias row fused), the "
+                      f"time class): {n_l} launches per step = every block's 6 Conv1D dW (bias gradient summed in the same GEMM), the "
                       "stacked caption K/V dW and the tied LM-head dW; achieved = sum of their algorithmic FLOPs "
                       f"/ sum of their in-step launch durations (HIP events around each launch, {n_probe_steps} steps run "
                       "right after the timed region)")
@@ -426,7 +426,9 @@ def main():
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S, E, Lyr, V),
                                                          0)},
-        "optimizer": "FusedAdamW " + (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks})"
+        "optimizer": "FusedAdamW " + ((f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks}), "
+                                       + ("scheduled by the native executor" if world == 1 else
+                                          "after each bucket's exchange (comm stream)"))
                                       if not args.no_overlap_optim else "after backward"),
         "world_size": world,
         "dp": {"backend": backend, "rehearsal": rehearse, "grad_comm": runner.dp.grad_comm,

@@ -40,6 +40,14 @@ class GemmDesc(C.Structure):
                 ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p)]
 
 
+class AdamWDesc(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("param_bf16", C.c_void_p), ("ranges", C.POINTER(C.c_int64)), ("n_ranges", C.c_int),
+                ("wte_begin", C.c_int64), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
+                ("eps", C.c_float), ("weight_decay", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float),
+                ("max_blocks", C.c_int)]
+
+
 class ModelDims(C.Structure):
     _fields_ = [("vocab", C.c_int), ("vocab_pad", C.c_int), ("n_embd", C.c_int), ("n_layer", C.c_int),
                 ("n_head", C.c_int), ("n_inner", C.c_int), ("n_positions", C.c_int), ("batch", C.c_int),
@@ -101,6 +109,7 @@ _SIGS = {
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),
     "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
+    "ergm_model_set_optimizer": (i32, [vp, vp]),
     "ergm_model_set_probe_list": (i32, [vp, i32, vp, vp, vp, i32]),
     "ergm_model_probe_count": (i32, [vp]),
     "ergm_model_set_row_flags": (i32, [vp, vp, i32]),

@@ -169,6 +169,14 @@ struct ergm_model_plan {
     int evl_n, evl_k;
     // diagnostic knock-out class of the launches being enqueued (ERGM_DIAG_SKIP, common.h)
     int diag_cls;
+    // executor-scheduled AdamW (ergm_model_set_optimizer): descriptor copy, its ranges, the optimizer stream
+    // and the main-stream marks it waits for (one per update of a step)
+    bool opt_on;
+    ergm_adamw_desc opt;
+    std::vector<int64_t> opt_ranges;
+    hipStream_t opt_s;
+    std::vector<hipEvent_t> ev_opt;
+    int opt_k;
     // dry-run sizing
     bool dry;
     size_t need;
@@ -636,6 +644,9 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->n_valid = nullptr;
     P->probe = 0;
     P->diag_cls = 0;
+    P->opt_on = false;
+    P->opt_s = nullptr;
+    P->opt_k = 0;
     P->ev_begin = P->ev_end = nullptr;
     P->evl_b = P->evl_e = nullptr;
     P->evl_flops = nullptr;
@@ -670,6 +681,12 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
             hipStreamDestroy(P->fwdx[c]);
         }
     }
+    if (P->opt_s) {
+        hipStreamSynchronize(P->opt_s);
+        hipStreamDestroy(P->opt_s);
+    }
+    for (auto e : P->ev_opt)
+        if (e) hipEventDestroy(e);
     if (P->ev_fork) hipEventDestroy(P->ev_fork);
     if (P->side) hipStreamDestroy(P->side);
     delete P;
@@ -1192,6 +1209,88 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
 
 }  // namespace
 
+extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_desc* o) {
+    ERGM_CHECK_ARG(P, "model_set_optimizer: null plan");
+    if (!o) {
+        P->opt_on = false;
+        return ERGM_OK;
+    }
+    const int L = P->d.n_layer;
+    ERGM_CHECK_ARG(o->param && o->grad && o->exp_avg && o->exp_avg_sq && o->ranges && o->n_ranges == L + 1,
+                   "model_set_optimizer: null buffer or n_ranges != n_layer + 1");
+    for (int k = 0; k <= L; ++k)
+        ERGM_CHECK_ARG(o->ranges[2 * k] >= 0 && o->ranges[2 * k + 1] > o->ranges[2 * k] &&
+                           o->ranges[2 * k] % 4 == 0 && o->ranges[2 * k + 1] % 4 == 0,
+                       "model_set_optimizer: range %d must be non-empty, 4-element aligned", k);
+    ERGM_CHECK_ARG(o->wte_begin >= 0 && o->wte_begin % 4 == 0, "model_set_optimizer: bad wte_begin");
+    if (!P->opt_s) {
+        if (hipStreamCreateWithFlags(&P->opt_s, hipStreamNonBlocking) != hipSuccess)
+            return fail(ERGM_EHIP, "model_set_optimizer: stream creation");
+        P->ev_opt.assign(L + 4, nullptr);
+        for (auto& e : P->ev_opt)
+            if (hipEventCreateWithFlags(&e, kSyncEv) != hipSuccess) return fail(ERGM_EHIP, "model_set_optimizer: event");
+    }
+    P->opt = *o;
+    P->opt_ranges.assign(o->ranges, o->ranges + 2 * (L + 1));
+    P->opt.ranges = P->opt_ranges.data();
+    P->opt_on = true;
+    return ERGM_OK;
+}
+
+namespace {
+// The optimizer stream waits for the work issued so far on `s` and, unless the stages already join the
+// side stream, for the side stream's weight-gradient mark `mark` (< 0: none).
+int opt_wait(ergm_model_plan* P, hipStream_t s, int mark) {
+    hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
+    if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
+        return fail(ERGM_EHIP, "model: optimizer stream wait");
+    if (mark >= 0 && hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) != hipSuccess)
+        return fail(ERGM_EHIP, "model: optimizer stream wait");
+    return ERGM_OK;
+}
+int opt_range(ergm_model_plan* P, int64_t a, int64_t b) {
+    const ergm_adamw_desc& o = P->opt;
+    void* sh = o.param_bf16 ? reinterpret_cast<__bf16*>(o.param_bf16) + a : nullptr;
+    return ergm_adamw_step(o.param + a, o.grad + a, o.exp_avg + a, o.exp_avg_sq + a, sh, (size_t)(b - a), o.lr, o.beta1,
+                           o.beta2, o.eps, o.weight_decay, o.step_size, o.bc2_sqrt, o.max_blocks, P->opt_s);
+}
+int opt_wte(ergm_model_plan* P, int select) {  // the tied wte's untouched (0) / touched (1) rows
+    const ergm_adamw_desc& o = P->opt;
+    const int64_t a = o.wte_begin, E = P->d.n_embd, rows = P->d.vocab_pad;
+    if (!P->row_flag) return select ? opt_range(P, a, a + rows * E) : ERGM_OK;
+    void* sh = o.param_bf16 ? reinterpret_cast<__bf16*>(o.param_bf16) + a : nullptr;
+    return ergm_adamw_rows(o.param + a, o.grad + a, o.exp_avg + a, o.exp_avg_sq + a, sh, (int)rows, (int)E, P->row_flag,
+                           select, o.lr, o.beta1, o.beta2, o.eps, o.weight_decay, o.step_size, o.bc2_sqrt, o.max_blocks,
+                           P->opt_s);
+}
+int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
+    if (!P->opt_on || P->dry) return ERGM_OK;
+    const int L = P->d.n_layer, i = L - 1 - l;
+    if (i >= 1) {  // block l+1's gradients (bucket i-1) are final: this stage and its weight-gradient mark
+        ERGM_TRY(opt_wait(P, s, l + 1));
+        ERGM_TRY(opt_range(P, P->opt.ranges[2 * (i - 1)], P->opt.ranges[2 * (i - 1) + 1]));
+    }
+    if (i == 1) {  // the LM-head part of the tied wte is final after its weight-gradient GEMM (mark L+1)
+        ERGM_TRY(opt_wait(P, s, L + 1));
+        ERGM_TRY(opt_wte(P, 0));
+    }
+    return ERGM_OK;
+}
+int opt_after_embed(ergm_model_plan* P, hipStream_t s) {
+    if (!P->opt_on || P->dry) return ERGM_OK;
+    const int L = P->d.n_layer;
+    ERGM_TRY(opt_wait(P, s, -1));  // the embedding stage joined every side-stream gradient
+    ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
+    if (L == 1) ERGM_TRY(opt_wte(P, 0));
+    ERGM_TRY(opt_range(P, P->opt.ranges[2 * L], P->opt.ranges[2 * L + 1]));
+    ERGM_TRY(opt_wte(P, 1));
+    hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
+    if (hipEventRecord(e, P->opt_s) != hipSuccess || hipStreamWaitEvent(s, e, 0) != hipSuccess)
+        return fail(ERGM_EHIP, "model: optimizer stream join");
+    return ERGM_OK;
+}
+}  // namespace
+
 extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_head: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_head: no training forward to differentiate");
@@ -1201,11 +1300,13 @@ extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale,
 extern "C" int ergm_model_backward_layer(ergm_model_plan* P, int layer, void* stream) {
     ERGM_CHECK_ARG(P && layer >= 0 && layer < P->d.n_layer, "model_backward_layer: bad layer");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_layer: no training forward to differentiate");
-    return do_backward_layer(P, layer, as_stream(stream));
+    ERGM_TRY(do_backward_layer(P, layer, as_stream(stream)));
+    return opt_after_layer(P, layer, as_stream(stream));
 }
 
 extern "C" int ergm_model_backward_embed(ergm_model_plan* P, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_embed: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_embed: no training forward to differentiate");
-    return do_backward_embed(P, as_stream(stream));
+    ERGM_TRY(do_backward_embed(P, as_stream(stream)));
+    return opt_after_embed(P, as_stream(stream));
 }

@@ -31,6 +31,8 @@ activations per shape).
 """
 from __future__ import annotations
 
+import os
+
 import weakref
 from collections import OrderedDict
 from dataclasses import dataclass
@@ -162,11 +164,14 @@ def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
     # flat.grad (no 600 MB accumulate pass); the flat input's returned gradient is None
     flat = model.flat
     if flat.grad is None:
-        post = None
+        post = native = None
         opt = model._overlap_opt
-        if opt is not None:
-            post = opt._backward_hook(flat, model)   # per-bucket AdamW, overlapped with backward
-        runner.backward(gl, post)                    # writes model.grad_buf
+        if opt is not None:  # per-bucket AdamW, overlapped with backward
+            if runner.dp.active or runner.compact_lookup or os.environ.get("ERGM_NATIVE_OPT", "1") == "0":
+                post = opt._backward_hook(flat, model)   # after each bucket's exchange (Python, comm stream)
+            else:
+                native = opt._native_desc(flat, model)   # scheduled by the executor
+        runner.backward(gl, post, native)            # writes model.grad_buf
         flat.grad = model.grad_buf
     elif flat.grad.data_ptr() == model.grad_buf.data_ptr():
         # accumulate semantics when the caller did not zero the gradient

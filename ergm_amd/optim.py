@@ -84,6 +84,39 @@ class FusedAdamW(torch.optim.Optimizer):
                                b2, eps, wd, t, nb)
         return post
 
+    def _native_desc(self, flat, model):
+        """Single process: the same per-bucket schedule run by the native executor
+        (ergm_model_set_optimizer) instead of Python hooks — an ergm_adamw_desc for this step, or None
+        when this optimizer does not own ``flat``."""
+        import ctypes as C
+        import math
+        from . import _lib as L
+        from .params import dp_buckets
+        group = self._group_of(flat)
+        if group is None:
+            return None
+        st = self._state(flat)
+        t = int(st["step"].item()) + 1
+        b1, b2 = group["betas"]
+        lay = model.layout
+        key = (id(model), lay.total)
+        if getattr(self, "_ranges_key", None) != key:
+            rs = dp_buckets(lay)[:lay.L] + [lay.seg["capwpe"]]
+            self._ranges = (C.c_int64 * (2 * len(rs)))(*[x for ab in rs for x in ab])
+            self._ranges_key = key
+        d = L.AdamWDesc()
+        d.param, d.grad = flat.data.data_ptr(), model.grad_buf.data_ptr()
+        d.exp_avg, d.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+        d.param_bf16 = model.flat_b16.data_ptr()
+        d.ranges, d.n_ranges = self._ranges, lay.L + 1
+        d.wte_begin = lay.seg["wte"][0]
+        d.lr, d.beta1, d.beta2, d.eps, d.weight_decay = group["lr"], b1, b2, group["eps"], group["weight_decay"]
+        d.step_size = group["lr"] / (1 - b1 ** t)
+        d.bc2_sqrt = math.sqrt(1 - b2 ** t)
+        d.max_blocks = int(self.overlap_blocks)
+        self._applied.add(id(flat))
+        return d
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

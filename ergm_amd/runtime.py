@@ -187,7 +187,7 @@ class ModelRunner:
         return logits, emo, loss
 
     # ---- backward -----------------------------------------------------------------------
-    def backward(self, grad_scale: Optional[torch.Tensor], post=None) -> None:
+    def backward(self, grad_scale: Optional[torch.Tensor], post=None, native_opt=None) -> None:
         """Writes every parameter gradient into self.grad (overwrite, not accumulate).  With a
         process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final.
 
@@ -199,6 +199,9 @@ class ModelRunner:
         lib = self.lib
         dp = self.dp
         dp.begin()
+        # single process: the executor runs the per-bucket AdamW schedule itself (ergm_model_set_optimizer)
+        L.check(lib.ergm_model_set_optimizer(self.plan, C.byref(native_opt) if native_opt is not None else None),
+                "ergm_model_set_optimizer")
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
         Lyr, E, Vp = self.layout.L, self.layout.E, self.layout.vocab_pad
         compact = self.compact_lookup

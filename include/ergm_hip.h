@@ -386,6 +386,31 @@ int ergm_model_backward_embed(ergm_model_plan* plan, void* stream);
  * draw for the concatenated batch).  Inference forwards (train = 0) never drop.                  */
 int ergm_model_set_dropout(ergm_model_plan* plan, float attn_p, float resid_p, float embd_p, uint64_t seed,
                            uint32_t offset, int batch_base);
+/* Executor-scheduled AdamW (single process).  With a descriptor set, the backward stages also launch the
+ * torch.optim.AdamW update (ergm_adamw_step / ergm_adamw_rows arithmetic) of each parameter range as soon as
+ * its gradient is final, on an optimizer stream of the plan that waits for the stage's data-gradient work and
+ * its weight-gradient mark; ergm_model_backward_embed joins that stream into the caller's, so every update is
+ * done, in stream order, when it returns.  Schedule: range k of `ranges` after stage k (0: head + block L-1,
+ * …, L-1: block 0, the last after the embedding stage), range L (caption K/V + wpe) after the embedding
+ * stage; the tied wte ([vocab_pad][n_embd] at wte_begin): the rows no lookup touched (ergm_model_set_row_flags)
+ * after the LM-head weight gradient (stage L-2), the touched rows after the embedding stage (all rows there
+ * when no row flags are set).  The descriptor (and its ranges) is copied; set it again every step (lr, step
+ * size); NULL disables.  Replaces ergm_amd's per-bucket Python hooks: one Python call per backward stage. */
+typedef struct {
+    float* param;             /* flat fp32 master */
+    const float* grad;        /* flat fp32 gradient */
+    float* exp_avg;
+    float* exp_avg_sq;
+    void* param_bf16;         /* flat bf16 shadow (refreshed by the update), or NULL */
+    const int64_t* ranges;    /* [n_ranges][2] element ranges [a, b) */
+    int n_ranges;             /* n_layer + 1 */
+    int64_t wte_begin;        /* element offset of the tied wte */
+    float lr, beta1, beta2, eps, weight_decay;
+    float step_size;          /* lr / (1 - beta1^t) */
+    float bc2_sqrt;           /* sqrt(1 - beta2^t) */
+    int max_blocks;           /* grid cap of each update, 0 = none */
+} ergm_adamw_desc;
+int ergm_model_set_optimizer(ergm_model_plan* plan, const ergm_adamw_desc* opt);
 /* Side-stream joins.  per_stage = 1 (default): the ordering guarantee above.  per_stage = 0: the
  * caller's stream does not wait for block l+1's weight gradients at the end of stage l (so the
  * data-gradient chain never idles behind the weight-gradient GEMMs); only backward_embed joins, after

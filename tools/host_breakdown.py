@@ -55,6 +55,36 @@ for _ in range(K):
     step(True)
 torch.cuda.synchronize()
 print({k: round(1000 * v / K, 3) for k, v in T.items()}, "total", round(1000 * sum(T.values()) / K, 3), "ms/step")
+# inside the autograd backward: time the runner's backward and the optimizer descriptor
+import ergm_amd.runtime as RT  # noqa: E402
+from ergm_amd import optim as OP  # noqa: E402
+inner = {"runner.backward": 0.0, "native_desc": 0.0}
+_rb, _nd = RT.ModelRunner.backward, OP.FusedAdamW._native_desc
+
+
+def rb(self, *a, **k):
+    t0 = time.perf_counter()
+    r = _rb(self, *a, **k)
+    inner["runner.backward"] += time.perf_counter() - t0
+    return r
+
+
+def nd(self, *a, **k):
+    t0 = time.perf_counter()
+    r = _nd(self, *a, **k)
+    inner["native_desc"] += time.perf_counter() - t0
+    return r
+
+
+RT.ModelRunner.backward, OP.FusedAdamW._native_desc = rb, nd
+for k in T:
+    T[k] = 0.0
+torch.cuda.synchronize()
+torch.cuda._sleep(int(2.4e9 * 0.2))
+for _ in range(K):
+    step(True)
+torch.cuda.synchronize()
+print({k: round(1000 * v / K, 3) for k, v in T.items()}, {k: round(1000 * v / K, 3) for k, v in inner.items()})
 # native calls alone: the runner's backward without the optimizer hooks
 runner = next(iter(model._runners.values()))
 gl = torch.ones(1, device=dev)
