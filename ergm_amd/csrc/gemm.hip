@@ -46,6 +46,8 @@ struct GemmArgs {
     DropSite drop;         // BIAS_RESID: dropout of the residual branch (src/model.py:245,266), rows m, cols n
     float* colsum;         // KM x KN, EPI_NONE: bias gradient alpha·Σ_k B[k][n] -> colsum[n] (nullptr: none)
     float* colsum_part;    // split-K: per-split partial column sums [z][N] (combined by splitk_reduce_kernel)
+    int xcd_split;         // split-K over 8 K slices, one per XCD: grid.x = 8·tiles, slice = blockIdx.x & 7, so
+                           // every tile of one K slice shares an XCD's L2 (pipelined kernel only)
 };
 
 template <int EPI, bool OUT_BF16>
@@ -331,12 +333,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int nwg = a.tiles_m * a.tiles_n;
-    const int id = xcd_remap(blockIdx.x, nwg);
+    // K slice zs: blockIdx.z, or (xcd_split) the XCD the workgroup runs on — workgroup b goes to XCD b % 8,
+    // so the tiles of one slice share that XCD's L2 and each operand slice is fetched once
+    const int zs = a.xcd_split ? (int)(blockIdx.x & 7) : (int)blockIdx.z;
+    const int id = a.xcd_split ? (int)(blockIdx.x >> 3) : xcd_remap(blockIdx.x, nwg);
+    if (id >= nwg) return;
     int tm, tn;
     if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
     else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = blockIdx.z * a.k_per_split;
+    const int kbeg = zs * a.k_per_split;
     const int kend = min(a.K, kbeg + a.k_per_split);
     const int nk = (kend - kbeg) / GEMM_BK;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     if constexpr (CS) {
         if (do_cs) {  // sum the four 16-lane rows (k groups), lane position (column) preserved
             const int lane = threadIdx.x & 63;
-            float* dst = a.slab ? a.colsum_part + (size_t)blockIdx.z * a.N : a.colsum;
+            float* dst = a.slab ? a.colsum_part + (size_t)zs * a.N : a.colsum;
             const float sc = a.slab ? 1.0f : alpha;  // split-K: the reduce kernel applies alpha
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
@@ -438,7 +444,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     if constexpr (DIRECT) {
         store_tile_direct<WGN, EPI, OUT_BF16, FM, FN, WM, WN>(a, acc, m0, n0, alpha);
     } else {
-        float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.M * a.N : nullptr;
+        float* slab = a.slab ? a.slab + (size_t)zs * a.M * a.N : nullptr;
         store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
     }
 }
@@ -697,6 +703,7 @@ struct GemmPlan {
     int cfg;    // index into kCfgs, or -1: register-staged fallback kernel
     int bm, bn;
     int split, kps;
+    bool xcd = false;  // split 8 with one K slice per XCD (GemmArgs::xcd_split)
 };
 
 static long tiles_of(int M, int N, int bm, int bn) { return (long)cdiv(M, bm) * cdiv(N, bn); }
@@ -812,6 +819,15 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
             // us in-step, profiles/r01_lmhead_probe.txt; c6s5 at C4, c6s4 at C5)
             p.cfg = 6;
             split = (int)std::max(1L, std::min(16L, 256 / std::max(1L, tiles_of(M, N, 256, 256))));
+            // opt-in (ERGM_XCD_SPLIT=1), at most 32 tiles (one XCD's CUs): 8 K slices, one per XCD, so each slice
+            // of both operands is fetched into one L2 once.  Measured slower for the LM-head dX at C2 (200 vs
+            // 177 us in-step, step 6.07 vs 5.95 ms): 192 workgroups with 1.24x the K steps each lose more than
+            // the 3x smaller operand re-fetch saves — the per-CU fill rate, not the fabric, bounds this GEMM.
+            static const bool xs_env = getenv("ERGM_XCD_SPLIT") && atoi(getenv("ERGM_XCD_SPLIT")) != 0;
+            if (xs_env && tiles_of(M, N, 256, 256) <= 32 && K >= 8 * 4096) {
+                split = 8;
+                p.xcd = true;
+            }
         } else if (K >= 4096 && t128 < 240 && d->split_k != 1) {
             p.cfg = 2;
             // weight gradients over T >= 4096 tokens (config 5): split only the smallest outputs
@@ -831,6 +847,7 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
     if (d->split_k > 1) split = d->split_k;
     int kps = cdiv(cdiv(K, split), GEMM_BK) * GEMM_BK;
     split = cdiv(K, kps);
+    if (p.xcd && split != 8) p.xcd = false;
     p.split = split;
     p.kps = kps;
     return p;
@@ -856,6 +873,7 @@ static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
                         true);
     (void)attr;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
+    if (a.xcd_split) grid = dim3(8 * a.tiles_m * a.tiles_n, 1, 1);  // split == 8, slice = XCD
     hipLaunchKernelGGL(split > 1 ? k_split : k_full, grid, dim3(nthreads), lds, s, a);
 }
 
@@ -1166,6 +1184,7 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0;
     a.colsum = cs_in ? d->bias_grad : nullptr;
     a.colsum_part = nullptr;
+    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 ? 1 : 0;
     if (p.split > 1) {
         size_t need = (size_t)p.split * d->M * d->N * sizeof(float) + (d->bias_grad ? (size_t)p.split * d->N * 4 : 0);
         ERGM_CHECK_ARG(ws && ws_bytes >= need, "ergm_gemm: split-K %d needs %zu workspace bytes (got %zu)", p.split,
