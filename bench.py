@@ -173,6 +173,8 @@ def main():
                          "1 = LM-head forward main launch, 2 = LM-head dX, 3 = LM-head dW, 4 = caption K/V GEMM")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
+    ap.add_argument("--defer-update", action="store_true",
+                    help="single process: run the block updates after the backward, overlapping the next forward")
     ap.add_argument("--no-gpu-only", dest="gpu_only", action="store_false",
                     help="skip the extra K steps enqueued behind a spin kernel (no host in the loop) that give "
                          "gpu_only_ms_per_step")
@@ -236,7 +238,8 @@ def main():
         cfg.attn_pdrop = cfg.resid_pdrop = cfg.embd_pdrop = args.pdrop
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
-    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim)
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim,
+                     defer=args.defer_update and world == 1)
     if args.adamw_blocks is not None:
         opt.overlap_blocks = args.adamw_blocks
     total = args.warmup + args.steps

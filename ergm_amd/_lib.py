@@ -45,7 +45,7 @@ class AdamWDesc(C.Structure):
                 ("param_bf16", C.c_void_p), ("ranges", C.POINTER(C.c_int64)), ("n_ranges", C.c_int),
                 ("wte_begin", C.c_int64), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
                 ("eps", C.c_float), ("weight_decay", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float),
-                ("max_blocks", C.c_int)]
+                ("max_blocks", C.c_int), ("defer", C.c_int)]
 
 
 class ModelDims(C.Structure):
@@ -110,6 +110,7 @@ _SIGS = {
     "ergm_model_destroy": (i32, [vp]),
     "ergm_model_set_probe": (i32, [vp, i32, vp, vp]),
     "ergm_model_set_optimizer": (i32, [vp, vp]),
+    "ergm_model_optimizer_join": (i32, [vp, vp]),
     "ergm_model_set_probe_list": (i32, [vp, i32, vp, vp, vp, i32]),
     "ergm_model_probe_count": (i32, [vp]),
     "ergm_model_set_row_flags": (i32, [vp, vp, i32]),

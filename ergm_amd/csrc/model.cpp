@@ -177,6 +177,8 @@ struct ergm_model_plan {
     hipStream_t opt_s;
     std::vector<hipEvent_t> ev_opt;
     int opt_k;
+    std::vector<hipEvent_t> ev_upd;  // deferred update of block l done (opt.defer)
+    std::vector<char> upd_pending;   // block l's deferred update not yet waited for by a forward
     // dry-run sizing
     bool dry;
     size_t need;
@@ -533,6 +535,7 @@ int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
 }
 
 int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_loss, int train, hipStream_t s);
+int wait_update(ergm_model_plan* P, int l, hipStream_t s);
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s);
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s);
 int do_backward_embed(ergm_model_plan* P, hipStream_t s);
@@ -687,6 +690,8 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
     }
     for (auto e : P->ev_opt)
         if (e) hipEventDestroy(e);
+    for (auto e : P->ev_upd)
+        if (e) hipEventDestroy(e);
     if (P->ev_fork) hipEventDestroy(P->ev_fork);
     if (P->side) hipStreamDestroy(P->side);
     delete P;
@@ -783,6 +788,7 @@ namespace {
 // sees the full-batch layout unchanged.
 int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
     DiagClass dc(P, 512);
+    ERGM_TRY(wait_update(P, l, s));  // a deferred optimizer update of this block's parameters
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int T = nb * S;
@@ -1016,6 +1022,8 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                                     P->emo_labels ? P->emo_sum : nullptr, P->n_valid + 1, out_loss, s));
     }
     P->have_fwd = train != 0;
+    if (!P->dry)
+        for (auto& f : P->upd_pending) f = 0;  // every block's forward waited for its update
     return check_launch("model_forward");
 }
 
@@ -1229,6 +1237,10 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
         P->ev_opt.assign(L + 4, nullptr);
         for (auto& e : P->ev_opt)
             if (hipEventCreateWithFlags(&e, kSyncEv) != hipSuccess) return fail(ERGM_EHIP, "model_set_optimizer: event");
+        P->ev_upd.assign(L, nullptr);
+        for (auto& e : P->ev_upd)
+            if (hipEventCreateWithFlags(&e, kSyncEv) != hipSuccess) return fail(ERGM_EHIP, "model_set_optimizer: event");
+        P->upd_pending.assign(L, 0);
     }
     P->opt = *o;
     P->opt_ranges.assign(o->ranges, o->ranges + 2 * (L + 1));
@@ -1266,7 +1278,7 @@ int opt_wte(ergm_model_plan* P, int select) {  // the tied wte's untouched (0) /
 int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
     if (!P->opt_on || P->dry) return ERGM_OK;
     const int L = P->d.n_layer, i = L - 1 - l;
-    if (i >= 1) {  // block l+1's gradients (bucket i-1) are final: this stage and its weight-gradient mark
+    if (i >= 1 && !P->opt.defer) {  // block l+1's gradients (bucket i-1) are final: this stage and its weight-gradient mark
         ERGM_TRY(opt_wait(P, s, l + 1));
         ERGM_TRY(opt_range(P, P->opt.ranges[2 * (i - 1)], P->opt.ranges[2 * (i - 1) + 1]));
     }
@@ -1287,9 +1299,33 @@ int opt_after_embed(ergm_model_plan* P, hipStream_t s) {
     hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
     if (hipEventRecord(e, P->opt_s) != hipSuccess || hipStreamWaitEvent(s, e, 0) != hipSuccess)
         return fail(ERGM_EHIP, "model: optimizer stream join");
+    if (P->opt.defer) {  // blocks 1 … L-1 (bucket L-1-l; bucket 0 also holds the head), in forward order
+        for (int l = 1; l < L; ++l) {
+            const int i = L - 1 - l;
+            ERGM_TRY(opt_range(P, P->opt.ranges[2 * i], P->opt.ranges[2 * i + 1]));
+            if (hipEventRecord(P->ev_upd[l], P->opt_s) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+            P->upd_pending[l] = 1;
+        }
+    }
     return ERGM_OK;
 }
+// The forward of block l on stream s waits for its deferred update (a no-op unless one is pending).
+int wait_update(ergm_model_plan* P, int l, hipStream_t s) {
+    if (P->dry || P->upd_pending.empty() || !P->upd_pending[l]) return ERGM_OK;
+    return hipStreamWaitEvent(s, P->ev_upd[l], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: update wait");
+}
 }  // namespace
+
+extern "C" int ergm_model_optimizer_join(ergm_model_plan* P, void* stream) {
+    ERGM_CHECK_ARG(P, "model_optimizer_join: null plan");
+    for (size_t l = 0; l < P->upd_pending.size(); ++l)
+        if (P->upd_pending[l]) {
+            if (hipStreamWaitEvent(as_stream(stream), P->ev_upd[l], 0) != hipSuccess)
+                return fail(ERGM_EHIP, "model_optimizer_join: hipStreamWaitEvent");
+            P->upd_pending[l] = 0;
+        }
+    return ERGM_OK;
+}
 
 extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_head: null plan");

@@ -31,6 +31,7 @@ activations per shape).
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import weakref
@@ -172,6 +173,8 @@ def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
             else:
                 native = opt._native_desc(flat, model)   # scheduled by the executor
         runner.backward(gl, post, native)            # writes model.grad_buf
+        if native is not None and native.defer:
+            model._deferred = runner                 # its block updates are still running (next forward waits)
         flat.grad = model.grad_buf
     elif flat.grad.data_ptr() == model.grad_buf.data_ptr():
         # accumulate semantics when the caller did not zero the gradient
@@ -209,6 +212,7 @@ class GPT2LMHeadModel(nn.Module):
         self._runners: Dict[tuple, ModelRunner] = {}
         self._b16_version = -1
         self._overlap_opt = None
+        self._deferred = None  # runner whose deferred optimizer updates no forward has waited for yet
         self._force_compact_lookup = False  # tests: the data-parallel wte path in one process
         self.process_group = process_group
         self._handle = id(self)
@@ -248,6 +252,7 @@ class GPT2LMHeadModel(nn.Module):
         self.load_state_dict(sd, strict=False)
 
     def state_dict(self, *args, destination=None, prefix="", keep_vars=False):
+        self.flush_deferred_()
         out = OrderedDict() if destination is None else destination
         for name in state_dict_names(self.layout):
             src = "transformer.wte.weight" if name == "lm_head.weight" else name
@@ -275,6 +280,15 @@ class GPT2LMHeadModel(nn.Module):
             r.dp.sharded.clear()
         return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
 
+    def flush_deferred_(self) -> None:
+        """Order the current stream after the optimizer's deferred block updates (FusedAdamW(defer=True)):
+        call before reading the parameters other than through a forward (which waits by itself)."""
+        r, self._deferred = self._deferred, None
+        if r is not None:
+            from . import _lib as L
+            L.check(r.lib.ergm_model_optimizer_join(r.plan, C.c_void_p(torch.cuda.current_stream(r.dev).cuda_stream)),
+                    "ergm_model_optimizer_join")
+
     @torch.no_grad()
     def consolidate_(self) -> None:
         """Data parallel with the sharded optimizer update (ZeRO-1, ergm_amd/dist.py): all-gather the
@@ -301,6 +315,7 @@ class GPT2LMHeadModel(nn.Module):
 
     @torch.no_grad()
     def refresh_bf16(self) -> None:
+        self.flush_deferred_()
         ops.cast_bf16(self.flat.data, self.flat_b16)
         self._b16_version = self.flat._version
 
@@ -401,6 +416,10 @@ class GPT2LMHeadModel(nn.Module):
         if self.flat._version != self._b16_version:
             self.refresh_bf16()  # weights changed outside FusedAdamW (e.g. torch.optim.AdamW)
         runner = self._runner(B, S, vis_rows, vis is not None)
+        if self._deferred is not None:  # the runner's own forward waits per block; another runner must join
+            if self._deferred is not runner:
+                self.flush_deferred_()
+            self._deferred = None
         V, Vp = self.config.vocab_size, self.layout.vocab_pad
         if torch.is_grad_enabled() and self.flat.requires_grad and (lab is not None or emo_lab is not None):
             loss3, logits, emo = torch.ops.ergm.train_step(self.flat, ids, tt, cap, vis, aud, lab, emo_lab, self._handle,

@@ -31,7 +31,7 @@ class FusedAdamW(torch.optim.Optimizer):
     """
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 model=None, overlap: bool = False):
+                 model=None, overlap: bool = False, defer: bool = False):
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         if not 0.0 <= eps:
@@ -42,6 +42,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.model = model  # when given, its bf16 shadow is refreshed in the same pass
         self._applied = set()
         self.overlap_blocks = 0  # grid cap of the overlapped per-bucket update (CUs it may occupy)
+        # single process, overlap=True: the block updates run after the backward, overlapping the next
+        # forward (which waits for each block's update before that block; ergm_model_optimizer_join)
+        self.defer = bool(defer)
         if overlap:
             if model is None:
                 raise ValueError("overlap=True needs model=")
@@ -114,8 +117,14 @@ class FusedAdamW(torch.optim.Optimizer):
         d.step_size = group["lr"] / (1 - b1 ** t)
         d.bc2_sqrt = math.sqrt(1 - b2 ** t)
         d.max_blocks = int(self.overlap_blocks)
+        d.defer = int(self.defer)
         self._applied.add(id(flat))
         return d
+
+    def state_dict(self):
+        if self.model is not None:
+            self.model.flush_deferred_()  # the moments of deferred block updates
+        return super().state_dict()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -137,8 +146,10 @@ class FusedAdamW(torch.optim.Optimizer):
                     if self.model is not None and p is self.model.flat:
                         self.model._b16_version = p._version
                     continue
-                if self.model is not None and p is self.model.flat and self.model.sharded:
-                    self.model.consolidate_()  # the full update needs every rank's master and moments
+                if self.model is not None and p is self.model.flat:
+                    self.model.flush_deferred_()  # pending deferred block updates first
+                    if self.model.sharded:
+                        self.model.consolidate_()  # the full update needs every rank's master and moments
                 t = int(st["step"].item())
                 shadow = None
                 if self.model is not None and p is self.model.flat:

@@ -409,8 +409,15 @@ typedef struct {
     float step_size;          /* lr / (1 - beta1^t) */
     float bc2_sqrt;           /* sqrt(1 - beta2^t) */
     int max_blocks;           /* grid cap of each update, 0 = none */
+    int defer;                /* 1: the updates of blocks 1 … L-1 (and the head) are launched after the embedding
+                               * stage instead, in forward order, and NOT joined: the next forward of the plan
+                               * waits for each block's update before that block (so they overlap the
+                               * latency-bound forward instead of the throughput-bound backward); anything else
+                               * that reads the parameters first calls ergm_model_optimizer_join */
 } ergm_adamw_desc;
 int ergm_model_set_optimizer(ergm_model_plan* plan, const ergm_adamw_desc* opt);
+/* Make `stream` wait for every deferred update still pending (no-op when none). */
+int ergm_model_optimizer_join(ergm_model_plan* plan, void* stream);
 /* Side-stream joins.  per_stage = 1 (default): the ordering guarantee above.  per_stage = 0: the
  * caller's stream does not wait for block l+1's weight gradients at the end of stage l (so the
  * data-gradient chain never idles behind the weight-gradient GEMMs); only backward_embed joins, after

@@ -139,29 +139,37 @@ def test_adamw_step_and_loss_decrease(gpu):
 
 @pytest.mark.parametrize("name", ["tiny_e64.npz", "small_e128_v500.npz"])
 def test_overlapped_adamw_matches_step_adamw(gpu, name):
-    """FusedAdamW(overlap=True) applies the same update during backward — per gradient bucket, the
-    tied wte split into untouched / lookup-touched rows — bitwise equal parameters, moments and bf16
-    shadow to the plain step() path over a scheduled LR."""
+    """FusedAdamW(overlap=True) applies the same update during backward — per gradient bucket (scheduled by
+    the executor, ergm_model_set_optimizer), the tied wte split into untouched / lookup-touched rows — and
+    with defer=True the block updates run after the backward, overlapping the next forward (which waits per
+    block; a forward of another batch shape joins them first): bitwise equal parameters, moments, bf16 shadow
+    and forward outputs to the plain step() path over a scheduled LR."""
     from ergm_amd.optim import get_polynomial_decay_schedule_with_warmup
     rec = _load(name)
     runs = []
-    for overlap in (False, True):
+    for overlap, defer in ((False, False), (True, False), (True, True)):
         _, _, _, model, batch = _setup(rec, gpu)
-        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=overlap)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=overlap, defer=defer)
         sched = get_polynomial_decay_schedule_with_warmup(opt, 2, 10, power=2.0)
-        for _ in range(3):
+        evals = []
+        for i in range(3):
             opt.zero_grad()
             out = _run(model, batch, gpu)
             opt.step()
             sched.step()
+            if i == 1:  # an inference forward of another shape (another runner) between steps
+                small = {k: v[:1].to(gpu) for k, v in batch.items() if k not in ("labels", "emotion_labels")}
+                with torch.no_grad():
+                    evals.append(model(**small).logits.float().clone())
+        model.flush_deferred_()
         torch.cuda.synchronize()
         st = opt.state[model.flat]
         runs.append((model.flat.detach().clone(), model.flat_b16.clone(), st["exp_avg"].clone(),
-                     st["exp_avg_sq"].clone(), float(st["step"]), out.loss.item()))
-    a, b = runs
-    for x, y in zip(a[:4], b[:4]):
-        assert torch.equal(x, y)
-    assert a[4] == b[4] == 3.0 and a[5] == b[5]
+                     st["exp_avg_sq"].clone(), evals[0], float(st["step"]), out.loss.item()))
+    for b in runs[1:]:
+        for x, y in zip(runs[0][:5], b[:5]):
+            assert torch.equal(x, y)
+        assert runs[0][5] == b[5] == 3.0 and runs[0][6] == b[6]
 
 
 @pytest.mark.parametrize("overlap", [False, True])
