@@ -271,6 +271,28 @@ def test_iemocap_shape_long_sequence_matches_oracle(gpu):
     _grad_gate(_grads(model), og)
 
 
+def test_full_c2_workload_matches_oracle(gpu):
+    """The bench workload end to end (BASELINE configs[1]: GPT-2-small L=12, E=768, H=12, V=50260, fusion
+    features, B=16, S=128, 5 turns) against the live oracle: loss, every logit, the emotion head and every
+    gradient within the bf16 gates."""
+    from ergm_amd.data import synthetic_batch
+    V, E, Lyr, H = 50260, 768, 12, 12
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, **NO_DROPOUT)
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    P0 = O.init_params(ocfg, seed=21)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    batch = synthetic_batch(16, 128, n_turns=5, feat_dim=E, seed=22)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss), (out.loss.item(), ref_loss)
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    assert abs(float(torch.log_softmax(out.emotion_logits.float().cpu(), -1).mean()) -
+               float(torch.log_softmax(ref["emotion_logits"].float(), -1).mean())) < 1e-2
+    _grad_gate(_grads(model), og)
+
+
 def test_full_vocab_lm_head_at_c2_token_count(gpu):
     """The LM head at C2's token count (T = 16·128 = 2048) over the real 50260-word vocabulary: the
     forward runs as the whole-round main launch (49152 columns) + the 1152-column tail launch, and the
