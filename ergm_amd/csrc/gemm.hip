@@ -738,12 +738,15 @@ static std::mutex g_over_mu;
 // automatic choice; profiles/r01_step_tune_*.json).  Runtime overrides take precedence.
 static constexpr GemmOverride kStepTuned[] = {
     // config 2 (GPT-2-small, B=16, S=128; forward GEMMs run per batch half, M = 1024)
-    {3072, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient
-    {768, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient
+    {3073, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient (+ the bias row)
+    {769, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient (+ the bias row)
+    {3072, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // the same with the in-GEMM bias column sums
+    {768, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},
     {1024, 2304, 768, ERGM_MK, ERGM_KN, 3, 1},   // c_attn forward
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
     {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
-    {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+    {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
+    {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1},
     {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
     {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
 };

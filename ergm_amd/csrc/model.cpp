@@ -29,6 +29,7 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
 int quant_weights_fp8(const WqJobs& J, hipStream_t s);
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
                    hipStream_t s);
+int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
@@ -72,6 +73,7 @@ struct ergm_model_plan {
     // Activations that feed a weight-gradient GEMM carry a constant ones column (index E or F) so the
     // dW GEMM over K+1 rows also yields the bias gradient (each bias is stored right after its weight).
     int XE, XF;
+    bool fused_bias;  // the ones-column layout holds (every bias right after its weight): dW over M+1 rows
     // activations
     float** resid;  // 3L+1 residual-stream tensors [T][E] f32
     std::vector<float*> resid_v;
@@ -442,7 +444,10 @@ struct DiagClass {  // tags the GEMMs enqueued in its scope for ERGM_DIAG_SKIP (
 };
 
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]) and its
-// bias gradient gB[N] = Σ_t dY[t][n], summed by the same GEMM from the dY fragments it stages.
+// bias gradient gB[N] = Σ_t dY[t][n].  With fused_bias the A operand's column M is all ones and gB == gW + M·N,
+// so one GEMM over M+1 rows writes [gW; gB] (the extra tile row runs beside the others); otherwise the GEMM
+// sums gB from the dY fragments it stages (ergm_gemm_desc.bias_grad: measured equal at C2 but +4 % step time
+// at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
 // kind: the dW's bit in dw_main (1 mlp c_proj, 2 c_fc, 4 cross c_proj, 8 cross q, 16 attn c_proj, 32 c_attn,
 // 64 caption K/V): set bits run on the (single) data-gradient stream, the rest on the side stream.
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
@@ -454,6 +459,8 @@ int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A,
     if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
     DiagClass dc(P, 0);
     Probe pr(P, 5, s, 2.0 * M * N * T + (double)N * T);
+    if (P->fused_bias)
+        return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
     return gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE, nullptr, nullptr, 0,
                 nullptr, 0, nullptr, nullptr, gB);
 }
@@ -551,6 +558,7 @@ extern "C" size_t ergm_model_workspace_size(const ergm_model_dims* dims) {
     P.L2E = 2 * dims->n_embd * dims->n_layer;
     size_t act = carve(&P, nullptr);
     P.dry = true;
+    P.fused_bias = false;  // size for the in-GEMM bias path (its split-K partials)
     P.need = ergm_embed_bwd_workspace_size(P.T);
     P.labels = P.emo_labels = nullptr;
     P.fwd2 = nullptr;
@@ -639,6 +647,32 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->need = 0;
     P->have_fwd = false;
     P->ln_pending = 0;
+    // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py lays the
+    // flat buffers out that way) and a ones column in the activations (set here; producers write columns
+    // < E / < F only); ERGM_FUSED_BIAS=0 selects the in-GEMM column sums.
+    {
+        const int64_t E = d.n_embd, F = d.n_inner;
+        const int64_t* o = P->p.layer_off;
+        auto follows = [&](int w, int b, int64_t K, int64_t N) { return o[b] == o[w] + K * N; };
+        P->fused_bias = follows(ERGM_T_ATTN_W, ERGM_T_ATTN_B, E, 3 * E) && follows(ERGM_T_APROJ_W, ERGM_T_APROJ_B, E, E) &&
+                        follows(ERGM_T_XQ_W, ERGM_T_XQ_B, E, E) && follows(ERGM_T_XPROJ_W, ERGM_T_XPROJ_B, E, E) &&
+                        follows(ERGM_T_FC_W, ERGM_T_FC_B, E, F) && follows(ERGM_T_MPROJ_W, ERGM_T_MPROJ_B, F, E) &&
+                        P->p.g_capkv_b == P->p.g_capkv_w + E * P->L2E;
+        if (const char* e = getenv("ERGM_FUSED_BIAS")) P->fused_bias = P->fused_bias && atoi(e) != 0;
+        int rc = ERGM_OK;
+        for (int l = 0; l < d.n_layer && rc == ERGM_OK; ++l) {
+            LayerActs& a = P->la[l];
+            const void* cols[5] = {a.ln1, a.lnx, a.ln2, a.ao, a.xo};
+            for (int i = 0; i < 5 && rc == ERGM_OK; ++i) rc = fill_ones_col((void*)cols[i], P->T, P->XE, d.n_embd, nullptr);
+            if (rc == ERGM_OK) rc = fill_ones_col(a.act, P->T, P->XF, d.n_inner, nullptr);
+        }
+        if (rc == ERGM_OK) rc = fill_ones_col(P->cap, P->T, P->XE, d.n_embd, nullptr);
+        if (rc == ERGM_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = fail(ERGM_EHIP, "model_create: sync");
+        if (rc != ERGM_OK) {
+            ergm_model_destroy(P);
+            return rc;
+        }
+    }
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
     P->row_flag = nullptr;

@@ -89,6 +89,36 @@ def test_gemm_split_k(gpu, split):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("M,N,K,split,cfg", [(768, 2304, 2048, 1, -1), (768, 768, 4096, 0, -1),
+                                               (200, 136, 1000, 1, -1), (256, 512, 2048, 3, -1),
+                                               (256, 512, 1024, 1, 0), (256, 512, 1024, 2, 2),
+                                               (256, 512, 1024, 1, 16)])
+def test_gemm_bias_grad(gpu, M, N, K, split, cfg):
+    """Weight gradient + its Conv1D bias gradient in one GEMM (ergm_gemm_desc.bias_grad): dW = Xᵀ·dY and
+    db = Σ_t dY[t] (the in-kernel column sums of the pipelined kernels, their split-K partials, and the
+    column-sum pass of the kernels without it: register-staged for K % 64 != 0, warp-specialised cfg 16),
+    against fp64; bitwise reproducible."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    X = (torch.randn(K, M, generator=g) * 0.5).to(gpu, torch.bfloat16)   # [tokens][in]  (KM)
+    dY = (torch.randn(K, N, generator=g) * 0.5).to(gpu, torch.bfloat16)  # [tokens][out] (KN)
+    L.check(L.load().ergm_gemm_tune(cfg, split if cfg >= 0 else 0), "tune")
+    try:
+        db = torch.full((N,), float("nan"), device=gpu)
+        dW = ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, split_k=split if cfg < 0 else 0, bias_grad=db)
+        db2 = torch.full((N,), float("nan"), device=gpu)
+        ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, split_k=split if cfg < 0 else 0, bias_grad=db2)
+    finally:
+        L.load().ergm_gemm_tune(-1, 0)
+    torch.cuda.synchronize()
+    ref_w = X.double().t() @ dY.double()
+    ref_b = dY.double().sum(0)
+    assert ((dW.double() - ref_w).norm() / ref_w.norm()).item() < 1e-5
+    assert ((db.double() - ref_b).abs() / (ref_b.abs() + 1.0)).max().item() < 1e-4
+    assert torch.equal(db, db2)
+    with pytest.raises(ValueError):  # other layouts / epilogues reject it
+        ops.gemm(X.t().contiguous(), dY, M, N, K, a_layout=L.MK, b_layout=L.KN, bias_grad=db)
+
+
 def test_gemm_epilogues(gpu):
     M, N, K = 256, 384, 192
     A = torch.randn(M, K, device=gpu).bfloat16()
