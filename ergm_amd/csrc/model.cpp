@@ -66,6 +66,17 @@ struct LayerW8 {
     int amax_n;
 };
 
+// one pending weight-gradient GEMM (dw_gemm / dw_flush)
+struct DwJob {
+    int M, N;
+    const __bf16* A;
+    int lda;
+    const __bf16* dY;
+    int ldy;
+    float* gW;
+    float* gB;
+};
+
 struct ergm_model_plan {
     ergm_model_dims d;
     ergm_model_params p;
@@ -110,6 +121,8 @@ struct ergm_model_plan {
     // after the head stage and joined by the embedding stage)
     int fwd_chains, bwd_chains;
     int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
+    bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
+    std::vector<DwJob> dw_pend;
     bool bwd_forked;
     hipStream_t fwd2;
     hipEvent_t ev_f2[3];
@@ -450,19 +463,35 @@ struct DiagClass {  // tags the GEMMs enqueued in its scope for ERGM_DIAG_SKIP (
 // at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
 // kind: the dW's bit in dw_main (1 mlp c_proj, 2 c_fc, 4 cross c_proj, 8 cross q, 16 attn c_proj, 32 c_attn,
 // 64 caption K/V): set bits run on the (single) data-gradient stream, the rest on the side stream.
+int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
+    const int T = P->T;
+    DiagClass dc(P, 0);
+    Probe pr(P, 5, s, 2.0 * j.M * j.N * T + (double)j.N * T);
+    if (P->fused_bias)
+        return gemm(P, s, j.M + 1, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE);
+    return gemm(P, s, j.M, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE,
+                nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, j.gB);
+}
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB, int kind = 0) {
-    const int T = P->T;
     const bool on_main = (P->dw_main & kind) && ch.n == 1;
-    if (!on_main) ERGM_TRY(fork_side(P, ch));
-    hipStream_t s = (P->dry || on_main) ? ch.s[0] : P->side;
     if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
-    DiagClass dc(P, 0);
-    Probe pr(P, 5, s, 2.0 * M * N * T + (double)N * T);
-    if (P->fused_bias)
-        return gemm(P, s, M + 1, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE);
-    return gemm(P, s, M, N, T, A, lda, ERGM_KM, dY, ldy, ERGM_KN, gW, N, ERGM_F32, ERGM_EPI_NONE, nullptr, nullptr, 0,
-                nullptr, 0, nullptr, nullptr, gB);
+    const DwJob j{M, N, A, lda, dY, ldy, gW, gB};
+    if (!on_main && P->dw_batch && !P->dry) {  // launched by the next dw_flush, behind one fork
+        P->dw_pend.push_back(j);
+        return ERGM_OK;
+    }
+    if (!on_main) ERGM_TRY(fork_side(P, ch));
+    return dw_launch(P, (P->dry || on_main) ? ch.s[0] : P->side, j);
+}
+// Launch the pending weight-gradient GEMMs on the side stream behind ONE fork from the data-gradient
+// chain(s) (every dY they read is complete there): one event record + wait instead of one per GEMM.
+int dw_flush(ergm_model_plan* P, const Chains& ch) {
+    if (P->dw_pend.empty()) return ERGM_OK;
+    ERGM_TRY(fork_side(P, ch));
+    for (const DwJob& j : P->dw_pend) ERGM_TRY(dw_launch(P, P->side, j));
+    P->dw_pend.clear();
+    return ERGM_OK;
 }
 
 // LayerNorm backward on the critical chain(s): rows [r0, r0 + rows) of the residual stream; its dγ/dβ
@@ -623,6 +652,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_BWD_CHAINS")) P->bwd_chains = atoi(e);
     P->dw_main = 0;
     if (const char* e = getenv("ERGM_DW_MAIN")) P->dw_main = atoi(e);
+    P->dw_batch = true;
+    if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -1140,6 +1171,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
                       R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
     ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), 2));
+    ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1162,6 +1194,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
     }
     ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), 8));
+    ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1184,6 +1217,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
     }
     ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B), 32));
+    ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
                       ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1235,6 +1269,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     }
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
     ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
+    ERGM_TRY(dw_flush(P, one));
     ERGM_TRY(side_mark(P, L + 2));
     ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                   ERGM_EPI_NONE));
