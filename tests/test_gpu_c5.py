@@ -102,6 +102,24 @@ def test_fp8_forward_training_step_matches_oracle(gpu, geom):
     _grad_gate(_grads(model), og, rtol=FP8_GRAD_RTOL)
 
 
+def test_fp8_full_depth_c5_geometry_matches_oracle(gpu):
+    """C5 at full depth (GPT-2-medium: 24 blocks, E=1024, H=16, the 50260-word vocabulary, 768-d features
+    projected to 1024, fp8 forward GEMMs), batch 8 of the bench's 32 to keep the CPU oracle at seconds:
+    the fp8 gates through all 24 blocks."""
+    V, E, Lyr, H, Fd = 50260, 1024, 24, 16, 768
+    ocfg, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=25)
+    cfg.fp8 = True
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    batch = synthetic_batch(8, 128, n_turns=5, feat_dim=Fd, seed=9)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    assert abs(out.loss.item() - ref["loss"].item()) <= FP8_LOSS_RTOL * abs(ref["loss"].item())
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= \
+        FP8_LOGIT_FRAC * ref["logits"].abs().max().item()
+    _grad_gate(_grads(model), og, rtol=FP8_GRAD_RTOL)
+
+
 def test_fp8_weights_follow_the_optimizer(gpu):
     """The fp8 weight copies are re-quantised at every forward: after optimizer steps the trained fp8
     model's forward is bit-identical to that of a fresh fp8 model loaded with the updated weights, and

@@ -293,6 +293,26 @@ def test_full_c2_workload_matches_oracle(gpu):
     _grad_gate(_grads(model), og)
 
 
+def test_full_c4_workload_matches_oracle(gpu):
+    """C4 end to end (BASELINE configs[3]: GPT-2-small, IEMOCAP shape S=512 with 20 turns, B=8, a
+    [B,197,768] BLIP-vision feature whose row 0 is injected, the tiled attention kernels, 3·B·S = 12288
+    lookups in the embedding sort) against the live oracle: loss, logits, every gradient."""
+    from ergm_amd.data import synthetic_batch
+    V, E, Lyr, H = 50260, 768, 12, 12
+    cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024, **NO_DROPOUT)
+    ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=1024)
+    P0 = O.init_params(ocfg, seed=31)
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=False)
+    batch = synthetic_batch(8, 512, n_turns=20, feat_dim=E, seed=32, visual_rows=197)
+    out = _run(model, batch, gpu)
+    ref, og = O.loss_and_grads(P0, ocfg, batch)
+    ref_loss = float(ref["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss), (out.loss.item(), ref_loss)
+    assert (out.logits.float().cpu() - ref["logits"]).abs().max().item() <= LOGIT_ATOL
+    _grad_gate(_grads(model), og)
+
+
 def test_full_vocab_lm_head_at_c2_token_count(gpu):
     """The LM head at C2's token count (T = 16·128 = 2048) over the real 50260-word vocabulary: the
     forward runs as the whole-round main launch (49152 columns) + the 1152-column tail launch, and the
