@@ -97,10 +97,12 @@ def test_buckets_partition_the_flat_buffer():
         assert len(inside) == 1, name
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16"])
-def test_dp2_matches_single_process_gradient(mode):
+@pytest.mark.parametrize("mode,world", [("fp32", 2), ("bf16", 2), ("bf16", 3)])
+def test_dp2_matches_single_process_gradient(mode, world):
+    """World 3 splits the batch of 4 unevenly (1, 1, 2 samples): the global-count normalisation and the
+    chunked exchange with a short last chunk."""
     path = os.path.join(tempfile.mkdtemp(), "g.pt")
-    mp.spawn(_worker, args=(2, _free_port(), path, mode), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), path, mode), nprocs=world, join=True)
     res = torch.load(path, weights_only=True)
     got = res["grad"]
     assert res["exchange_ok"]
@@ -111,9 +113,10 @@ def test_dp2_matches_single_process_gradient(mode):
     err = ((got - want).norm() / want.norm()).item()
     # fp32: exact up to summation order; bf16: one rounding of each rank's gradient and of the sum
     assert err < (1e-5 if mode == "fp32" else 4e-3), err
-    # bytes each rank moves per step: bf16 is half of fp32 (to within the chunk padding)
-    layout_bytes = 2 * (2 - 1) * layout.total * (4 if mode == "fp32" else 2) // 2
-    assert abs(res["bytes"] - 1004 * (4 if mode == "fp32" else 2) - layout_bytes) <= 64 * 16 * 4
+    # bytes each rank moves per step: 2·(W-1)/W of the buffer, bf16 half of fp32 (to within the chunk padding)
+    es = 4 if mode == "fp32" else 2
+    want_bytes = 2 * (world - 1) * (layout.total + 1004) * es / world
+    assert abs(res["bytes"] - want_bytes) <= 64 * 16 * 4 * world, (res["bytes"], want_bytes)
 
 
 def test_grad_comm_mode_validated():
@@ -161,9 +164,11 @@ def _zero_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_zero1_sharded_update_matches_replicated():
+@pytest.mark.parametrize("world", [2, 3])
+def test_zero1_sharded_update_matches_replicated(world):
+    """World 3: chunks of ceil(n/3) rounded up to 8 elements, the last rank's shard shorter (or empty)."""
     path = os.path.join(tempfile.mkdtemp(), "z.pt")
-    mp.spawn(_zero_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    mp.spawn(_zero_worker, args=(world, _free_port(), path), nprocs=world, join=True)
     r = torch.load(path, weights_only=True)
     assert r["ok"]
     assert r["sharded"] == [(0, 1000), (1000, 2000), (2000, 4064)] and r["none"] == []
