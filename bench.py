@@ -172,6 +172,8 @@ def main():
                     help="roofline probe: 5 = every weight-gradient GEMM launch (the dominant time class, default); "
                          "1 = LM-head forward main launch, 2 = LM-head dX, 3 = LM-head dW, 4 = caption K/V GEMM")
     ap.add_argument("--no-fp8", action="store_true", help="c5: run the forward GEMMs in bf16 instead of fp8")
+    ap.add_argument("--torch-metrics", action="store_true",
+                    help="per-step metrics with framework ops instead of the executor's loss finalisation")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
     ap.add_argument("--defer-update", action="store_true",
                     help="single process: run the block updates after the backward, overlapping the next forward")
@@ -257,6 +259,10 @@ def main():
         aud_hidden = (0.1 * torch.randn(B, 400, Fd, generator=torch.Generator().manual_seed(7 + rank))).to(dev)
     loss_acc = torch.zeros(2, device=dev)
     correct = torch.zeros(1, device=dev, dtype=torch.int64)
+    # the trainer's per-step metrics (src/main.py:158-169), kept on device (no host sync) and accumulated by
+    # the executor's loss finalisation (--torch-metrics: the equivalent framework ops after each step)
+    if not args.torch_metrics:
+        model.set_train_metrics(loss_acc, correct)
 
     def step():
         if aud_hidden is not None:
@@ -266,10 +272,10 @@ def main():
         out.loss.backward()
         opt.step()
         sched.step()
-        # the trainer's per-step metrics (src/main.py:158-169), kept on device (no host sync)
-        loss_acc[0] += out.loss.detach()
-        loss_acc[1] += out.loss_lm
-        correct.add_((out.emotion_logits.argmax(-1) == kw["emotion_labels"]).sum())
+        if args.torch_metrics:
+            loss_acc[0] += out.loss.detach()
+            loss_acc[1] += out.loss_lm
+            correct.add_((out.emotion_logits.argmax(-1) == kw["emotion_labels"]).sum())
         return out
 
     for _ in range(args.warmup):

@@ -124,6 +124,7 @@ _SIGS = {
     "ergm_model_backward_layer": (i32, [vp, i32, vp]),
     "ergm_model_backward_embed": (i32, [vp, vp]),
     "ergm_model_set_side_joins": (i32, [vp, i32]),
+    "ergm_model_set_metrics": (i32, [vp, vp, vp]),
     "ergm_model_stage_wait": (i32, [vp, i32, vp]),
 }
 EXPORTED = sorted(_SIGS)

@@ -32,7 +32,8 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // Diagnostic knock-out switches (ERGM_DIAG_SKIP bitmask; never set in normal runs: the results are wrong):
 // 1 = weight-gradient GEMMs, 2 = LayerNorm dγ/dβ reductions, 4 = AdamW passes, 8 = attention backward,
 // 16 = LayerNorm forward (block LayerNorms), 32 = LayerNorm backward, 64 = attention forward, 128 = LM-head
-// GEMMs, 256 = cross-entropy, 512 = block forward GEMMs, 1024 = block data-gradient GEMMs.
+// GEMMs, 256 = cross-entropy, 512 = block forward GEMMs, 1024 = block data-gradient GEMMs, 2048 = the
+// embedding stage's caption K/V GEMMs (dW and dX over the stacked projection).
 // Used only to measure what a class of launches costs the concurrent step.
 int diag_skip();
 

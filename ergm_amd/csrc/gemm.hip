@@ -321,8 +321,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // Pipelined variant: NS-stage LDS ring filled by LDS-DMA (GldsTile, tiles.h), counted waits, raw barrier.
+// The body takes its workgroup index `bid` (the tile, before the XCD remap) so that a grouped launch can run
+// several problems in one grid (gemm_dw2_kernel).
 template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
+__device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid) {
     constexpr int NW = WGM * WGN;
     constexpr int WM = BM / WGM, WN = BN / WGN;
     constexpr int FM = WM / 16, FN = WN / 16;
@@ -335,8 +337,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     const int nwg = a.tiles_m * a.tiles_n;
     // K slice zs: blockIdx.z, or (xcd_split) the XCD the workgroup runs on — workgroup b goes to XCD b % 8,
     // so the tiles of one slice share that XCD's L2 and each operand slice is fetched once
-    const int zs = a.xcd_split ? (int)(blockIdx.x & 7) : (int)blockIdx.z;
-    const int id = a.xcd_split ? (int)(blockIdx.x >> 3) : xcd_remap(blockIdx.x, nwg);
+    const int zs = a.xcd_split ? (bid & 7) : (int)blockIdx.z;
+    const int id = a.xcd_split ? (bid >> 3) : xcd_remap(bid, nwg);
     if (id >= nwg) return;
     int tm, tn;
     if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
@@ -446,6 +448,31 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
     } else {
         float* slab = a.slab ? a.slab + (size_t)zs * a.M * a.N : nullptr;
         store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
+    }
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT>(a, blockIdx.x);
+}
+
+// Two weight-gradient GEMMs (KM x KN, f32 out, no split) in ONE launch: workgroups [0, b1) run problem 0
+// (those past its tile count exit), [b1, b1 + tiles of problem 1) run problem 1.  A block's dW GEMMs
+// are issued in pairs on the side stream, and each alone has 126-168 tiles — fewer than the 256 CUs —
+// so as two launches the pair's second half waits for the first to drain; as one grid both fill the chip
+// together.  b1 is a multiple of 8, so the XCD remap of problem 1 sees the same block -> XCD pattern.
+struct GemmArgs2 {
+    GemmArgs a[2];
+    int b1;
+};
+template <int BM, int BN, int WGM, int WGN, int NS>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_dw2_kernel(GemmArgs2 g) {
+    const int b = blockIdx.x;
+    if (b < g.b1) {
+        if (b >= g.a[0].tiles_m * g.a[0].tiles_n) return;
+        gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false>(g.a[0], b);
+    } else {
+        gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false>(g.a[1], b - g.b1);
     }
 }
 
@@ -1124,8 +1151,45 @@ extern "C" int ergm_gemm_trace(int on, int* shapes, int max_shapes) {
     return n;
 }
 
-extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, void* C, void* ws,
-                         size_t ws_bytes, void* stream) {
+namespace ergm {
+// Kernel arguments of one planned GEMM (split-K slabs are set by the caller).
+static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B, void* C, const GemmPlan& p) {
+    GemmArgs a;
+    a.A = reinterpret_cast<const __bf16*>(A);
+    a.B = reinterpret_cast<const __bf16*>(B);
+    a.C = C;
+    a.M = d->M; a.N = d->N; a.K = d->K;
+    a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+    a.alpha = d->alpha; a.alpha_dev = d->alpha_dev;
+    a.bias = d->bias; a.aux = d->aux; a.ld_aux = d->ld_aux;
+    a.aux_out = d->aux_out; a.ld_aux_out = d->ld_aux_out;
+    a.tiles_m = cdiv(d->M, p.bm); a.tiles_n = cdiv(d->N, p.bn);
+    // stream the larger operand once: walk along the dimension of the smaller operand
+    a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
+    a.k_per_split = p.kps;
+    a.slab = nullptr;
+    a.a_scale = a.b_scale = nullptr;
+    a.drop = drop_site_of(d->dropout, d->N);
+    // the vocabulary-wide bf16 logits (206 MB at C2) are streamed out with non-temporal stores so they
+    // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
+    // profiles/r01_overlap_experiments.txt #14); ERGM_NT_STORE=0 disables (A/B)
+    static const int nt_env = getenv("ERGM_NT_STORE") ? atoi(getenv("ERGM_NT_STORE")) : 1;
+    // ... and so are the f32 weight gradients (A = activationsᵀ), consumed later by the optimizer / the
+    // all-reduce (C5 +0.4-0.8 %, C2 neutral: #17)
+    a.nt_store = nt_env && ((d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
+                            (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE));
+    // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
+    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0;
+    a.colsum = cs_in ? d->bias_grad : nullptr;
+    a.colsum_part = nullptr;
+    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 ? 1 : 0;
+    return a;
+}
+}  // namespace ergm
+
+namespace ergm {
+// Argument checks of ergm_gemm (also applied to each problem of a grouped launch).
+static int validate_desc(const ergm_gemm_desc* d, const void* A, const void* B, const void* C) {
     ERGM_CHECK_ARG(d && A && B && C, "ergm_gemm: null argument");
     ERGM_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "ergm_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
     // k-contiguous operands are read in 8-element chunks along K; with both operands k-major (rows = k,
@@ -1156,38 +1220,19 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
                                      d->c_dtype == ERGM_F32),
                    "ergm_gemm: bias_grad needs a_layout KM, b_layout KN, epilogue NONE and f32 C");
 
+    return ERGM_OK;
+}
+}  // namespace ergm
+
+extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, void* C, void* ws,
+                         size_t ws_bytes, void* stream) {
+    ERGM_TRY(validate_desc(d, A, B, C));
+    const int e = d->epilogue;
     trace_shape(d);
     GemmPlan p = plan_gemm(d);
-    GemmArgs a;
-    a.A = reinterpret_cast<const __bf16*>(A);
-    a.B = reinterpret_cast<const __bf16*>(B);
-    a.C = C;
-    a.M = d->M; a.N = d->N; a.K = d->K;
-    a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
-    a.alpha = d->alpha; a.alpha_dev = d->alpha_dev;
-    a.bias = d->bias; a.aux = d->aux; a.ld_aux = d->ld_aux;
-    a.aux_out = d->aux_out; a.ld_aux_out = d->ld_aux_out;
-    a.tiles_m = cdiv(d->M, p.bm); a.tiles_n = cdiv(d->N, p.bn);
-    // stream the larger operand once: walk along the dimension of the smaller operand
-    a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
-    a.k_per_split = p.kps;
-    a.slab = nullptr;
-    a.a_scale = a.b_scale = nullptr;
-    a.drop = drop_site_of(d->dropout, d->N);
-    // the vocabulary-wide bf16 logits (206 MB at C2) are streamed out with non-temporal stores so they
-    // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
-    // profiles/r01_overlap_experiments.txt #14); ERGM_NT_STORE=0 disables (A/B)
-    static const int nt_env = getenv("ERGM_NT_STORE") ? atoi(getenv("ERGM_NT_STORE")) : 1;
-    // ... and so are the f32 weight gradients (A = activationsᵀ), consumed later by the optimizer / the
-    // all-reduce (C5 +0.4-0.8 %, C2 neutral: #17)
-    a.nt_store = nt_env && ((d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
-                            (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE));
+    GemmArgs a = make_args(d, A, B, C, p);
+    const bool cs_in = a.colsum != nullptr;
     hipStream_t s = as_stream(stream);
-    // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
-    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0;
-    a.colsum = cs_in ? d->bias_grad : nullptr;
-    a.colsum_part = nullptr;
-    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 ? 1 : 0;
     if (p.split > 1) {
         size_t need = (size_t)p.split * d->M * d->N * sizeof(float) + (d->bias_grad ? (size_t)p.split * d->N * 4 : 0);
         ERGM_CHECK_ARG(ws && ws_bytes >= need, "ergm_gemm: split-K %d needs %zu workspace bytes (got %zu)", p.split,
@@ -1219,3 +1264,66 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
                            d->alpha_dev, d->bias_grad);
     return check_launch("ergm_gemm");
 }
+
+namespace ergm {
+template <int C>
+static void launch_dw2_cfg(const GemmArgs2& g, int nblocks, hipStream_t s) {
+    constexpr PipeCfg c = kCfgs[C];
+    static_assert(c.np == 0 && !c.direct, "grouped dW launch: pipelined kernels with the staged epilogue only");
+    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
+    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns>;
+    static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
+    (void)attr;
+    hipLaunchKernelGGL(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
+}
+
+// Two weight-gradient GEMMs (a_layout KM, b_layout KN, epilogue NONE, f32 C) in one launch when both plan
+// to the same unsplit pipelined configuration; ERGM_EUNSUPPORTED (nothing launched) otherwise, and the caller
+// issues them one by one.  launch = false: only the check.  Same kernel body and tile order as ergm_gemm: the results are bit-identical.
+int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const void* const B[2], void* const C[2],
+                 void* stream, bool launch) {
+    for (int i = 0; i < 2; ++i) {
+        ERGM_TRY(validate_desc(d[i], A[i], B[i], C[i]));
+        if (d[i]->a_layout != ERGM_KM || d[i]->b_layout != ERGM_KN || d[i]->epilogue != ERGM_EPI_NONE ||
+            d[i]->c_dtype != ERGM_F32 || d[i]->split_k > 1 || !pipe_ok(d[i]))
+            return ERGM_EUNSUPPORTED;
+    }
+    GemmPlan p[2] = {plan_gemm(d[0]), plan_gemm(d[1])};
+    const int cfg = p[0].cfg;
+    if (cfg < 0 || cfg >= 16 || p[1].cfg != cfg || p[0].split != 1 || p[1].split != 1 || p[0].xcd || p[1].xcd ||
+        kCfgs[cfg].np != 0 || kCfgs[cfg].direct)
+        return ERGM_EUNSUPPORTED;
+    // only pairs whose problems each leave CUs idle: grouping two chip-filling GEMMs measured slower (C5:
+    // 264 + 288 tiles, step +1.2 %); C2's pairs (150 + 168, 156 + 156 tiles) gain 0.4 %
+    if (tiles_of(d[0]->M, d[0]->N, p[0].bm, p[0].bn) >= 256 || tiles_of(d[1]->M, d[1]->N, p[1].bm, p[1].bn) >= 256)
+        return ERGM_EUNSUPPORTED;
+    if (!launch) return ERGM_OK;
+    trace_shape(d[0]);
+    trace_shape(d[1]);
+    GemmArgs2 g;
+    for (int i = 0; i < 2; ++i) g.a[i] = make_args(d[i], A[i], B[i], C[i], p[i]);
+    const int n0 = g.a[0].tiles_m * g.a[0].tiles_n, n1 = g.a[1].tiles_m * g.a[1].tiles_n;
+    g.b1 = (n0 + 7) & ~7;
+    const int nb = g.b1 + n1;
+    hipStream_t s = as_stream(stream);
+    switch (cfg) {
+        case 0: launch_dw2_cfg<0>(g, nb, s); break;
+        case 1: launch_dw2_cfg<1>(g, nb, s); break;
+        case 2: launch_dw2_cfg<2>(g, nb, s); break;
+        case 3: launch_dw2_cfg<3>(g, nb, s); break;
+        case 4: launch_dw2_cfg<4>(g, nb, s); break;
+        case 5: launch_dw2_cfg<5>(g, nb, s); break;
+        case 6: launch_dw2_cfg<6>(g, nb, s); break;
+        case 7: launch_dw2_cfg<7>(g, nb, s); break;
+        case 8: launch_dw2_cfg<8>(g, nb, s); break;
+        case 9: launch_dw2_cfg<9>(g, nb, s); break;
+        case 10: launch_dw2_cfg<10>(g, nb, s); break;
+        case 11: launch_dw2_cfg<11>(g, nb, s); break;
+        case 12: launch_dw2_cfg<12>(g, nb, s); break;
+        case 13: launch_dw2_cfg<13>(g, nb, s); break;
+        case 14: launch_dw2_cfg<14>(g, nb, s); break;
+        default: launch_dw2_cfg<15>(g, nb, s); break;
+    }
+    return check_launch("gemm_dw_pair");
+}
+}  // namespace ergm

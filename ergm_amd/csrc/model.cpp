@@ -38,6 +38,11 @@ int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, i
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
                              float* const* dgamma, float* const* dbeta, hipStream_t s);
+int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
+                          const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
+                          const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s);
+int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const void* const B[2], void* const C[2],
+                 void* stream, bool launch);
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
                  int V, hipStream_t s, const DropSite& drop);
@@ -122,6 +127,7 @@ struct ergm_model_plan {
     int fwd_chains, bwd_chains;
     int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
     bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
+    bool dw_group;  // ... and a qualifying pair as ONE grouped launch (gemm_dw_pair)
     std::vector<DwJob> dw_pend;
     bool bwd_forked;
     hipStream_t fwd2;
@@ -163,6 +169,8 @@ struct ergm_model_plan {
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
     const float *vis, *aud;
     const int* n_valid;  // [0] valid LM labels, [1] valid emotion labels (global under DP)
+    float* metric_loss = nullptr;       // ergm_model_set_metrics: [0] += loss, [1] += LM loss per training forward
+    int64_t* metric_correct = nullptr;  // += emotion argmax hits per training forward
     bool have_fwd;
     // dropout (src/model.py:142,245,266,506): probabilities, seed and forward number set by the caller
     // (ergm_model_set_dropout) for the next training forward; `drop_on` is latched by that forward and
@@ -463,14 +471,39 @@ struct DiagClass {  // tags the GEMMs enqueued in its scope for ERGM_DIAG_SKIP (
 // at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
 // kind: the dW's bit in dw_main (1 mlp c_proj, 2 c_fc, 4 cross c_proj, 8 cross q, 16 attn c_proj, 32 c_attn,
 // 64 caption K/V): set bits run on the (single) data-gradient stream, the rest on the side stream.
+double dw_flops(const ergm_model_plan* P, const DwJob& j) { return 2.0 * j.M * j.N * P->T + (double)j.N * P->T; }
 int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
     const int T = P->T;
     DiagClass dc(P, 0);
-    Probe pr(P, 5, s, 2.0 * j.M * j.N * T + (double)j.N * T);
+    Probe pr(P, 5, s, dw_flops(P, j));
     if (P->fused_bias)
         return gemm(P, s, j.M + 1, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE);
     return gemm(P, s, j.M, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE,
                 nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, j.gB);
+}
+// Two pending weight-gradient GEMMs as ONE grouped launch (gemm_dw_pair) when they plan to the same unsplit
+// configuration: each alone has fewer tiles than the chip has CUs (ERGM_DW_GROUP=0: two launches).
+// Returns ERGM_EUNSUPPORTED when the pair does not qualify (nothing launched).
+int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJob& j1) {
+    if (!P->dw_group) return ERGM_EUNSUPPORTED;
+    const int T = P->T;
+    ergm_gemm_desc g[2];
+    const DwJob* j[2] = {&j0, &j1};
+    for (int i = 0; i < 2; ++i) {
+        memset(&g[i], 0, sizeof(g[i]));
+        g[i].M = P->fused_bias ? j[i]->M + 1 : j[i]->M;
+        g[i].N = j[i]->N; g[i].K = T; g[i].lda = j[i]->lda; g[i].ldb = j[i]->ldy; g[i].ldc = j[i]->N;
+        g[i].a_layout = ERGM_KM; g[i].b_layout = ERGM_KN; g[i].c_dtype = ERGM_F32; g[i].epilogue = ERGM_EPI_NONE;
+        g[i].alpha = 1.0f;
+        g[i].bias_grad = P->fused_bias ? nullptr : j[i]->gB;
+    }
+    const ergm_gemm_desc* d[2] = {&g[0], &g[1]};
+    const void* A[2] = {j0.A, j1.A};
+    const void* B[2] = {j0.dY, j1.dY};
+    void* C[2] = {j0.gW, j1.gW};
+    ERGM_TRY(gemm_dw_pair(d, A, B, C, s, false));
+    Probe pr(P, 5, s, dw_flops(P, j0) + dw_flops(P, j1));
+    return gemm_dw_pair(d, A, B, C, s, true);
 }
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
             float* gW, float* gB, int kind = 0) {
@@ -489,7 +522,13 @@ int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A,
 int dw_flush(ergm_model_plan* P, const Chains& ch) {
     if (P->dw_pend.empty()) return ERGM_OK;
     ERGM_TRY(fork_side(P, ch));
-    for (const DwJob& j : P->dw_pend) ERGM_TRY(dw_launch(P, P->side, j));
+    size_t i = 0;
+    for (; i + 1 < P->dw_pend.size(); i += 2) {
+        const int r = dw_launch_pair(P, P->side, P->dw_pend[i], P->dw_pend[i + 1]);
+        if (r == ERGM_EUNSUPPORTED) break;
+        ERGM_TRY(r);
+    }
+    for (; i < P->dw_pend.size(); ++i) ERGM_TRY(dw_launch(P, P->side, P->dw_pend[i]));
     P->dw_pend.clear();
     return ERGM_OK;
 }
@@ -654,6 +693,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_DW_MAIN")) P->dw_main = atoi(e);
     P->dw_batch = true;
     if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
+    P->dw_group = true;
+    if (const char* e = getenv("ERGM_DW_GROUP")) P->dw_group = atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -805,6 +846,13 @@ extern "C" int ergm_model_set_dropout(ergm_model_plan* P, float attn_p, float re
     return ERGM_OK;
 }
 
+extern "C" int ergm_model_set_metrics(ergm_model_plan* P, float* loss_acc, int64_t* correct) {
+    ERGM_CHECK_ARG(P, "model_set_metrics: null plan");
+    P->metric_loss = loss_acc;
+    P->metric_correct = correct;
+    return ERGM_OK;
+}
+
 extern "C" int ergm_model_set_side_joins(ergm_model_plan* P, int per_stage) {
     ERGM_CHECK_ARG(P, "model_set_side_joins: null plan");
     P->per_stage_join = per_stage != 0;
@@ -851,9 +899,13 @@ namespace {
 // kernel is row- (or batch-) separable, so two such chains over disjoint halves of the batch run
 // concurrently on two streams and write disjoint rows of the same activation buffers — the backward
 // sees the full-batch layout unchanged.
-int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
+// `part` selects one launch group (0-10, in chain order: LN1, c_attn, attention, attn c_proj, LN_x, q,
+// cross-attention, cross c_proj, LN2, c_fc, mlp c_proj) so that the caller can interleave the chains
+// launch by launch; -1 issues the whole block.
+int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part = -1) {
     DiagClass dc(P, 512);
-    ERGM_TRY(wait_update(P, l, s));  // a deferred optimizer update of this block's parameters
+    auto on = [part](int k) { return part < 0 || part == k; };
+    if (on(0)) ERGM_TRY(wait_update(P, l, s));  // a deferred optimizer update of this block's parameters
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, L = d.n_layer, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int T = nb * S;
@@ -880,71 +932,84 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb) {
     uint8_t* qf = f8 && !P->dry ? P->qf + r0 * F : nullptr;
     float* sa = f8 && !P->dry ? P->sa + r0 : nullptr;
     float* sf = f8 && !P->dry ? P->sf + r0 : nullptr;
-    if (w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
+    if (on(0) && w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
     // dropout sites of this block over the chain's rows (src/model.py:142 probabilities, :245 / :266
     // residual branches)
     const ergm_dropout dr_attn = resid_drop(P, 3 * l + 1, b0), dr_cross = resid_drop(P, 3 * l + 2, b0),
                        dr_mlp = resid_drop(P, 3 * l + 3, b0);
     const ergm_dropout dp_self = attn_drop(P, l, 0, b0), dp_cross = attn_drop(P, l, 1, b0);
     // self-attention sub-block (src/model.py:297-309)
-    if (!P->dry)
+    if (on(0) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
                                   d.eps, s, qa, E, sa));
-    if (f8)
-        ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
-                       ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
-    else
-        ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
-                      ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
-    if (!P->dry)
+    if (on(1)) {
+        if (f8)
+            ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
+                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+        else
+            ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
+                          ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+    }
+    if (on(2) && !P->dry)
         ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, nb, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
                                &dp_self, attn_bits(P, l, 0, b0), s));
-    if (f8) {
-        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
-        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, &dr_attn));
-    } else {
-        ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, nullptr, &dr_attn));
+    if (on(3)) {
+        if (f8) {
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
+                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, &dr_attn));
+        } else {
+            ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, nullptr, &dr_attn));
+        }
     }
     // cross-attention over caption embeddings (src/model.py:311-329)
-    if (!P->dry)
+    if (on(4) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
                                   d.eps, s, qa, E, sa));
-    if (f8)
-        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E, ERGM_BF16,
-                       ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
-    else
-        ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
-                      ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+    if (on(5)) {
+        if (f8)
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E, ERGM_BF16,
+                           ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+        else
+            ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
+                          ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+    }
     const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
-    if (l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
-    if (!P->dry)
+    if (on(6) && l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
+    if (on(6) && !P->dry)
         ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
                                attn_bits(P, l, 1, b0), s));
-    if (f8) {
-        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
-        ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, &dr_cross));
-    } else {
-        ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, nullptr, &dr_cross));
+    if (on(7)) {
+        if (f8) {
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
+                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, &dr_cross));
+        } else {
+            ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, nullptr, &dr_cross));
+        }
     }
     // MLP (src/model.py:331-334, 262-267)
-    if (!P->dry)
+    if (on(8) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
                                   d.eps, s, qa, E, sa));
     if (f8) {
-        ERGM_TRY(gemm8(P, s, T, F, E, qa, sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
-                       ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-        if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
-        ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E, ERGM_F32,
-                       ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, &dr_mlp));
+        if (on(9)) {
+            ERGM_TRY(gemm8(P, s, T, F, E, qa, sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
+                           ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
+        }
+        if (on(10))
+            ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E, ERGM_F32,
+                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, &dr_mlp));
     } else {
-        ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF, ERGM_BF16,
-                      ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-        ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
-                      ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, nullptr, &dr_mlp));
+        if (on(9))
+            ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF,
+                          ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
+        if (on(10))
+            ERGM_TRY(gemm(P, s, T, E, F, a.act, P->XF, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_KN, x3, E, ERGM_F32,
+                          ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, nullptr, &dr_mlp));
     }
     (void)L;
     return ERGM_OK;
@@ -1050,8 +1115,22 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         if (P->f8)
             for (int l = 1; l < L; ++l) ERGM_TRY(quant_layer_weights(P, l, ss));
     }
-    for (int l = 0; l < L; ++l)  // enqueue block by block, alternating chains
-        for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
+    // Enqueue order: launch by launch, alternating chains (ERGM_FWD_INTERLEAVE=0: block by block).  The
+    // forward's kernels are short, so the host's enqueue pace can set the GPU's: enqueued a block at a
+    // time, the chains ran one block after the other instead of side by side.
+    static const bool interleave = [] {
+        const char* e = getenv("ERGM_FWD_INTERLEAVE");
+        return !(e && e[0] == '0');
+    }();
+    for (int l = 0; l < L; ++l) {
+        if (interleave && nchain > 1) {
+            for (int part = 0; part <= 10; ++part)
+                for (int c = 0; c < nchain; ++c)
+                    ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], part));
+        } else {
+            for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
+        }
+    }
     for (int c = 1; c < nchain && !P->dry; ++c)
         if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
             return fail(ERGM_EHIP, "model: chain join");
@@ -1083,8 +1162,14 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     }
     if (P->labels || P->emo_labels) {
         if (!P->labels) ERGM_TRY(hipMemsetAsync(P->row_loss, 0, (size_t)T * 4, s) == hipSuccess ? ERGM_OK : ERGM_EHIP);
-        ERGM_TRY(ergm_loss_finalize(P->row_loss, T, P->labels ? P->n_valid : nullptr,
-                                    P->emo_labels ? P->emo_sum : nullptr, P->n_valid + 1, out_loss, s));
+        if (train && (P->metric_loss || P->metric_correct))
+            ERGM_TRY(loss_finalize_metrics(P->row_loss, T, P->labels ? P->n_valid : nullptr,
+                                           P->emo_labels ? P->emo_sum : nullptr, P->n_valid + 1, out_loss,
+                                           P->metric_loss, P->emo_labels ? P->metric_correct : nullptr, emo_logits,
+                                           P->emo_labels, B, 7, s));
+        else
+            ERGM_TRY(ergm_loss_finalize(P->row_loss, T, P->labels ? P->n_valid : nullptr,
+                                        P->emo_labels ? P->emo_sum : nullptr, P->n_valid + 1, out_loss, s));
     }
     P->have_fwd = train != 0;
     if (!P->dry)
@@ -1268,6 +1353,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
         }
     }
     // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
+    DiagClass dc(P, 2048);
     ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
     ERGM_TRY(dw_flush(P, one));
     ERGM_TRY(side_mark(P, L + 2));
@@ -1355,13 +1441,17 @@ int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
         ERGM_TRY(opt_wait(P, s, L + 1));
         ERGM_TRY(opt_wte(P, 0));
     }
+    if (l == 0 && !P->opt.defer) {  // block 0 (bucket L-1): final with this stage's mark, not the embedding stage
+        ERGM_TRY(opt_wait(P, s, 0));
+        ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
+    }
     return ERGM_OK;
 }
 int opt_after_embed(ergm_model_plan* P, hipStream_t s) {
     if (!P->opt_on || P->dry) return ERGM_OK;
     const int L = P->d.n_layer;
     ERGM_TRY(opt_wait(P, s, -1));  // the embedding stage joined every side-stream gradient
-    ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
+    if (P->opt.defer) ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
     if (L == 1) ERGM_TRY(opt_wte(P, 0));
     ERGM_TRY(opt_range(P, P->opt.ranges[2 * L], P->opt.ranges[2 * L + 1]));
     ERGM_TRY(opt_wte(P, 1));

@@ -220,15 +220,41 @@ __global__ __launch_bounds__(256) void emotion_dw_kernel(const __bf16* __restric
         if (c < C) dW[(size_t)c * E + e] = acc[c];
 }
 
+// The trainer's running metrics (src/main.py:158-169: loss.item() sums and emotion argmax accuracy),
+// accumulated on the device by the loss finalisation instead of a string of small framework kernels.
+struct MetricAcc {
+    float* loss_acc;             // [0] += total loss, [1] += LM loss (nullptr: off)
+    unsigned long long* correct;  // += #(argmax(emo_logits[b]) == emo_labels[b])
+    const float* emo_logits;     // [B][C]
+    const int64_t* emo_labels;   // [B]
+    int B, C;
+};
+
 __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restrict__ row_loss, int T,
                                                             const int* __restrict__ n_valid,
                                                             const float* __restrict__ emo_sum,
-                                                            const int* __restrict__ n_emo, float* __restrict__ out) {
+                                                            const int* __restrict__ n_emo, float* __restrict__ out,
+                                                            MetricAcc acc) {
     __shared__ float red[4];
+    __shared__ int hits[4];
     float s = 0.f;
     for (int i = threadIdx.x; i < T; i += 256) s += row_loss[i];
     s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    int h = 0;
+    if (acc.correct && acc.emo_logits && acc.emo_labels) {
+        for (int b = threadIdx.x; b < acc.B; b += 256) {  // torch argmax: the first index of the maximum
+            const float* r = acc.emo_logits + (size_t)b * acc.C;
+            int best = 0;
+            for (int c = 1; c < acc.C; ++c)
+                if (r[c] > r[best]) best = c;
+            h += (int64_t)best == acc.emo_labels[b];
+        }
+    }
+    h = (int)wave_sum((float)h);
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = s;
+        hits[threadIdx.x >> 6] = h;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         float lm = ((red[0] + red[1]) + red[2]) + red[3];
@@ -239,6 +265,11 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(const float* __restr
         out[0] = lm;
         out[1] = emo;
         out[2] = lm + emo;
+        if (acc.loss_acc) {
+            acc.loss_acc[0] += lm + emo;
+            acc.loss_acc[1] += lm;
+        }
+        if (acc.correct) *acc.correct += (unsigned long long)(hits[0] + hits[1] + hits[2] + hits[3]);
     }
 }
 
@@ -297,6 +328,18 @@ extern "C" int ergm_loss_finalize(const float* row_loss, int T, const int* n_val
     ERGM_CHECK_ARG(row_loss && out && T > 0, "loss_finalize: bad argument");
     ERGM_CHECK_ARG(!emo_loss_sum || n_valid_emo, "loss_finalize: the emotion loss needs its valid count");
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, as_stream(stream), row_loss, T, n_valid_global,
-                       emo_loss_sum, n_valid_emo, out);
+                       emo_loss_sum, n_valid_emo, out, MetricAcc{});
     return check_launch("loss_finalize");
 }
+
+namespace ergm {
+// ergm_loss_finalize that also accumulates the trainer metrics (ergm_model_set_metrics).
+int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
+                          const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
+                          const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s) {
+    MetricAcc acc{loss_acc, reinterpret_cast<unsigned long long*>(correct), emo_logits, emo_labels, B, C};
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, row_loss, T, n_valid_global, emo_loss_sum,
+                       n_valid_emo, out, acc);
+    return check_launch("loss_finalize");
+}
+}  // namespace ergm

@@ -210,6 +210,7 @@ class GPT2LMHeadModel(nn.Module):
         self.grad_buf = torch.zeros(n, dtype=torch.float32, device=dev)
         self._tmp = None
         self._runners: Dict[tuple, ModelRunner] = {}
+        self._train_metrics = None  # set_train_metrics
         self._b16_version = -1
         self._overlap_opt = None
         self._deferred = None  # runner whose deferred optimizer updates no forward has waited for yet
@@ -352,8 +353,25 @@ class GPT2LMHeadModel(nn.Module):
                             has_feat, self.process_group)
             if self._force_compact_lookup:
                 r.force_compact_lookup()
+            if self._train_metrics is not None:
+                r.set_metrics(*self._train_metrics)
             self._runners[key] = r
         return r
+
+    def set_train_metrics(self, loss_acc: Optional[torch.Tensor], correct: Optional[torch.Tensor] = None) -> None:
+        """Accumulate the trainer's per-step metrics on the device (src/main.py:158-169): every training
+        forward adds its loss to ``loss_acc[0]``, its LM loss to ``loss_acc[1]`` (fp32, 2 elements) and its
+        emotion argmax hits to ``correct`` (int64, 1 element), inside the loss finalisation — the same
+        numbers as ``loss_acc += (out.loss, out.loss_lm)`` and ``correct += (argmax == labels).sum()`` with
+        no extra launches.  ``None`` turns it off."""
+        if loss_acc is not None:
+            if loss_acc.dtype != torch.float32 or loss_acc.numel() < 2 or not loss_acc.is_contiguous():
+                raise ValueError("loss_acc must be a contiguous fp32 tensor of 2 elements")
+            if correct is not None and (correct.dtype != torch.int64 or correct.numel() < 1):
+                raise ValueError("correct must be an int64 tensor of 1 element")
+        self._train_metrics = None if loss_acc is None else (loss_acc, correct)
+        for r in self._runners.values():
+            r.set_metrics(loss_acc, correct if loss_acc is not None else None)
 
     def forward(self, input_ids=None, past_key_values=None, attention_mask=None, token_type_ids=None,
                 position_ids=None, head_mask=None, inputs_embeds=None, encoder_hidden_states=None,

@@ -106,6 +106,11 @@ class ModelRunner:
         if self.compact_lookup:
             self._setup_compact()
 
+    def set_metrics(self, loss_acc: Optional[torch.Tensor], correct: Optional[torch.Tensor]) -> None:
+        """Device-side trainer metrics of every training forward (ergm_model_set_metrics)."""
+        self._metrics = (loss_acc, correct)  # keep alive
+        L.check(self.lib.ergm_model_set_metrics(self.plan, _p(loss_acc), _p(correct)), "ergm_model_set_metrics")
+
     def _setup_compact(self):
         Vp, E = self.layout.vocab_pad, self.layout.E
         cap = min(Vp, self.dp.world * 3 * self.B * self.S)

@@ -426,6 +426,11 @@ int ergm_model_optimizer_join(ergm_model_plan* plan, void* stream);
  * its_stream) after the stage that finalises it was enqueued; stage L+1 = the LM-head (tied wte)
  * weight gradient, L+2 = the caption K/V / projection weight gradients.                             */
 int ergm_model_set_side_joins(ergm_model_plan* plan, int per_stage);
+/* Trainer metrics on the device (src/main.py:158-169: the running sum of loss.item() and the emotion
+ * argmax accuracy): when set, every training forward adds its total loss to loss_acc[0], its LM loss to
+ * loss_acc[1] and its number of samples with argmax(emotion_logits) == emotion_labels (first maximum, as
+ * torch.argmax) to *correct, in the loss finalisation (no extra launch).  nullptr pointers: off.      */
+int ergm_model_set_metrics(ergm_model_plan* plan, float* loss_acc, int64_t* correct);
 int ergm_model_stage_wait(ergm_model_plan* plan, int stage, void* stream);
 
 /* Kernel probe for in-loop timing: while set, the executor records `ev_begin` / `ev_end`

@@ -457,6 +457,56 @@ def test_backward_chains_are_bitwise_the_single_chain(gpu, monkeypatch, B, S):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("B,S", [(16, 128), (3, 32)])
+def test_grouped_weight_gradient_launches_are_bitwise_the_separate_ones(gpu, monkeypatch, B, S):
+    """The block's weight-gradient GEMMs issued as grouped two-problem launches (gemm_dw_pair) give
+    bitwise the gradients of one launch per GEMM (ERGM_DW_GROUP=0); B = 16, S = 128 is C2's token count
+    on a narrow model, where the pairs qualify."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    res = []
+    for group in ("0", "1"):
+        monkeypatch.setenv("ERGM_DW_GROUP", group)
+        ocfg, P0, model = _small_model(gpu, S, seed=61)
+        batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=62, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+        out = _run(model, batch, gpu)
+        res.append((out.loss.detach().clone(), model.flat.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_device_train_metrics_match_framework_ops(gpu):
+    """GPT2LMHeadModel.set_train_metrics: the loss finalisation accumulates loss, LM loss and emotion argmax
+    hits (src/main.py:158-169) exactly as the equivalent torch ops on the step outputs; eval forwards and
+    set_train_metrics(None) add nothing."""
+    rec = _load("tiny_e64.npz")
+    _, _, _, model, batch = _setup(rec, gpu)
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    acc = torch.zeros(2, device=gpu)
+    hits = torch.zeros(1, device=gpu, dtype=torch.int64)
+    model.set_train_metrics(acc, hits)
+    ref_acc, ref_hits = torch.zeros(2, device=gpu, dtype=torch.float64), 0
+    for k in range(3):
+        model.flat.grad = None
+        out = model(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                    emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+                    auds=kw["audio_feat"])
+        out.loss.backward()
+        ref_acc[0] += out.loss.detach().double()
+        ref_acc[1] += out.loss_lm.double()
+        ref_hits += int((out.emotion_logits.argmax(-1) == kw["emotion_labels"]).sum())
+    torch.cuda.synchronize()
+    assert torch.allclose(acc.double(), ref_acc, rtol=1e-6, atol=0) and int(hits) == ref_hits
+    model.eval()
+    with torch.no_grad():
+        model(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+              emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+              auds=kw["audio_feat"])
+    model.train()
+    model.set_train_metrics(None)
+    torch.cuda.synchronize()
+    assert torch.allclose(acc.double(), ref_acc, rtol=1e-6, atol=0) and int(hits) == ref_hits
+
+
 def test_custom_op_registration_and_torch_compile(gpu):
     """The fused step is the torch.library custom op ergm::train_step (+ its backward op), opaque to
     autograd and torch.compile: a compiled model gives the eager loss, logits and gradients."""
