@@ -342,6 +342,25 @@ def main():
         for (b, e, _, _, fl), n in zip(plist, counts):
             durs += [b[k].elapsed_ms(e[k]) for k in range(n)]
             flops += [fl[k] for k in range(n)]
+        if os.environ.get("ERGM_BENCH_PHASES"):  # diagnostics: device time of forward / backward per step
+            ph = []
+            for _ in range(5):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                ev[0].record()
+                out = model(**kw)
+                ev[1].record()
+                opt.zero_grad()
+                out.loss.backward()
+                opt.step()
+                sched.step()
+                ev[2].record()
+                ph.append(ev)
+            torch.cuda.synchronize()
+            res = {"forward_ms": sum(e[0].elapsed_time(e[1]) for e in ph) / len(ph),
+                   "backward_opt_ms": sum(e[1].elapsed_time(e[2]) for e in ph) / len(ph),
+                   "step_ms": sum(e[0].elapsed_time(e[2]) for e in ph) / len(ph)}
+            with open(os.environ["ERGM_BENCH_PHASES"], "w") as f:
+                json.dump(res, f)
         if os.environ.get("ERGM_BENCH_FWD_DETAIL"):  # the same for the block forward GEMMs (list probe 6)
             NF = 6 * 2 * cfg.n_layer + 8
             fl = []

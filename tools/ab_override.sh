@@ -2,7 +2,7 @@
 # A/B of GEMM configuration overrides inside the bench step: tools/ab_override.sh "label:M,N,K,al,bl,cfg,split[ ...]" ...
 # ("label:" alone = the built-in table); two interleaved rounds.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-for rep in 1 2; do
+for rep in $(seq 1 ${ROUNDS:-2}); do
   for v in "$@"; do
     l=${v%%:*}; o=${v#*:}
     if [ -z "$o" ]; then
