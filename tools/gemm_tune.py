@@ -150,6 +150,8 @@ def main():
 
         row["times"]["auto"] = run_cfg(-1, 0)
         cfgs = range(len(CFGS)) if not quick else [0, 1, 3, 4, 7]
+        if "--auto-only" in sys.argv:  # only the automatic plan of every shape (A/B of two builds)
+            cfgs = []
         for cfg in cfgs:
             bm, bn = CFGS[cfg]
             tiles = -(-M // bm) * -(-N // bn)
@@ -162,7 +164,7 @@ def main():
                 except Exception as ex:  # noqa: BLE001
                     row["times"][f"c{cfg}s{sp}"] = None
                     print("  fail", name, cfg, sp, ex, flush=True)
-        valid = {k: v for k, v in row["times"].items() if v is not None and k != "auto"}
+        valid = {k: v for k, v in row["times"].items() if v is not None and (k != "auto" or not cfgs)}
         best = min(valid, key=valid.get)
         row["best"] = best
         total_best += valid[best] * cnt
