@@ -213,7 +213,18 @@ def main():
     dev = torch.device("cuda", local)
     pg = None
     backend = None
-    if world > 1:
+    # host-cost hook (one-GPU box): ERGM_BENCH_FAKE_PG=N runs ONE process as rank 0 of a torch "fake" process
+    # group of N ranks, whose collectives do nothing — the whole data-parallel schedule (per-bucket casts,
+    # chunk sums, sharded AdamW, master sync) is enqueued and run on the GPU, only the wire is missing, so the
+    # step's host enqueue and GPU time under DP can be measured (results and utterances/s not meaningful)
+    fake_world = int(os.environ.get("ERGM_BENCH_FAKE_PG", "0"))
+    if fake_world > 1 and world == 1:
+        import torch.distributed as dist
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+        dist.init_process_group("fake", rank=0, world_size=fake_world, store=FakeStore())
+        pg, backend, world = dist.group.WORLD, "fake", fake_world
+        args.gpus = fake_world
+    if world > 1 and pg is None:
         import torch.distributed as dist
         backend = args.backend or ("gloo" if rehearse else "nccl")
         if backend == "nccl":
@@ -305,6 +316,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    sync0 = sum(r.host_sync_s for r in model._runners.values())
     t0 = time.perf_counter()
     for i in range(args.steps):
         if args.probe != 5:
@@ -312,6 +324,7 @@ def main():
             _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
         step()
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (≈ dt when host-bound)
+    t_sync = sum(r.host_sync_s for r in model._runners.values()) - sync0  # of it: waiting (DP row count)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -478,6 +491,8 @@ def main():
                "sharded_optimizer": runner.dp.zero} if world > 1 else None,
         "host_enqueue_ms_per_step": host_ms,
         "host_enqueue_ms_per_step_in_timed_loop": round(1000.0 * t_enq / args.steps, 3),
+        # under DP the host also blocks once per step on the compact lookup's row count: the rest is host work
+        "host_busy_ms_per_step_in_timed_loop": round(1000.0 * (t_enq - t_sync) / args.steps, 3),
         "train_metrics": {"mean_loss": round(metrics[0] / total, 4),
                           "emotion_acc": round(metrics[1] / (B * total), 4)},
     }

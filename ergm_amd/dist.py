@@ -57,6 +57,11 @@ class DPSync:
         self._pool32 = None        # fp32 gather buffer (consolidate_)
         self.bytes_per_step = 0    # gradient bytes this rank sent in the last backward (bench report)
         self.zero = self.grad_comm == "bf16" and os.environ.get("ERGM_DP_ZERO", "1") != "0"
+        # consecutive block buckets exchanged together (ERGM_DP_MERGE, default 2): every exchange costs the
+        # host ~0.15 ms of Python / ctypes / collective calls, which at 14 buckets per step left the host at
+        # ~90 % of the GPU step under DP (bench ERGM_BENCH_FAKE_PG); two blocks per exchange halve that
+        self.merge = max(1, int(os.environ.get("ERGM_DP_MERGE", "2")))
+        self._pend_a: Optional[int] = None
         # flat ranges [a, b) whose last update ran shard-wise (stale outside this rank's chunk)
         self.sharded: set = set()
         self._master = None        # fp32 master whose directly-read elements stay replicated (set_master)
@@ -118,6 +123,7 @@ class DPSync:
     def begin(self) -> None:
         self._works = []
         self.bytes_per_step = 0
+        self._pend_a = None
 
     def _buffers(self, chunk: int, dev) -> Tuple[torch.Tensor, ...]:
         W = self.world
@@ -284,6 +290,13 @@ class DPSync:
         if not self.active and post is None:
             return
         a, b = self.buckets[k]
+        last_block = len(self.buckets) - 2  # the final bucket (embeddings) is never merged
+        if self.merge > 1 and k <= last_block:
+            if self._pend_a is None:
+                self._pend_a = a
+            if (k + 1) % self.merge != 0 and k != last_block:
+                return  # exchanged with the next block's bucket (contiguous: blocks are stored in this order)
+            a, self._pend_a = self._pend_a, None
         # the side stream waits for the collectives; no host synchronisation
         self.enqueue(grad, lambda: self.reduce_then(grad, a, b, post, shadow), k, wait)
 

@@ -11,6 +11,7 @@ stream while later blocks are still being differentiated.
 from __future__ import annotations
 
 import ctypes as C
+import time
 from typing import Optional
 
 import torch
@@ -102,6 +103,7 @@ class ModelRunner:
         # ranks' union of touched rows (ergm_model_set_lookup_compact); the dense LM-head part is
         # all-reduced early, during the block backward.  compact_lookup can be forced for testing.
         self.compact_lookup = self.dp.active
+        self.host_sync_s = 0.0  # host time spent waiting for the compact row count (DP), diagnostics
         self._compact_ready = False
         if self.compact_lookup:
             self._setup_compact()
@@ -234,7 +236,9 @@ class ModelRunner:
 
         def wte_lookup_rows():  # lookup part of the touched rows, then their update
             if compact:
+                t0 = time.perf_counter()
                 self._ev_count.synchronize()  # recorded right after the forward: long complete
+                self.host_sync_s += time.perf_counter() - t0
                 n = int(self.row_count_host[0]) * E
                 if dp.active and n:
                     dp.reduce_(self.compact[:n])

@@ -124,7 +124,7 @@ def test_grad_comm_mode_validated():
         DPSync(None, [], grad_comm="fp16")
 
 
-def _zero_worker(rank, world, port, out_path):
+def _zero_worker(rank, world, port, out_path, merge=1):
     """The sharded update (ZeRO-1) against the replicated one, same gradients: a plain SGD-like
     ``post`` stands in for the optimizer; after consolidate_ the master, the gradient and the bf16
     shadow must be bitwise those of the replicated bf16 exchange."""
@@ -142,6 +142,7 @@ def _zero_worker(rank, world, port, out_path):
         shadow = p.to(torch.bfloat16)
         dp = DPSync(dist.group.WORLD, buckets, grad_comm="bf16")
         dp.zero = zero
+        dp.merge = merge
         dp.set_master(p, [(10, 30), (990, 1010), (3000, 3100)])  # "directly read" fp32 ranges
 
         def post(a, b):
@@ -164,11 +165,14 @@ def _zero_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_zero1_sharded_update_matches_replicated(world):
-    """World 3: chunks of ceil(n/3) rounded up to 8 elements, the last rank's shard shorter (or empty)."""
+@pytest.mark.parametrize("world,merge", [(2, 1), (3, 1), (2, 2), (3, 2)])
+def test_zero1_sharded_update_matches_replicated(world, merge):
+    """World 3: chunks of ceil(n/3) rounded up to 8 elements, the last rank's shard shorter (or empty).
+    merge = 2 (the default): consecutive block buckets exchanged together, the last (embedding) bucket
+    alone — the same per-element arithmetic, so the same numbers."""
     path = os.path.join(tempfile.mkdtemp(), "z.pt")
-    mp.spawn(_zero_worker, args=(world, _free_port(), path), nprocs=world, join=True)
+    mp.spawn(_zero_worker, args=(world, _free_port(), path, merge), nprocs=world, join=True)
     r = torch.load(path, weights_only=True)
     assert r["ok"]
-    assert r["sharded"] == [(0, 1000), (1000, 2000), (2000, 4064)] and r["none"] == []
+    want = [(0, 1000), (1000, 2000), (2000, 4064)] if merge == 1 else [(0, 2000), (2000, 4064)]
+    assert r["sharded"] == want and r["none"] == []
