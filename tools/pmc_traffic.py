@@ -71,20 +71,24 @@ def main():
                               "algorithmic_bytes": alg, "ratio": (fb + wb) / alg}
     # the weight-gradient GEMM class (bench.py's roofline): every KM x KN pipelined GEMM dispatch; mean
     # bytes per launch over the class against the mean algorithmic bytes of its C2 launches
-    dwk = [k for k in fetch if "gemm_pipe_kernel<" in k and ", true, true, " in k]
+    dwk = [k for k in fetch if ("gemm_pipe_kernel<" in k and ", true, true, " in k) or "gemm_dw2_kernel<" in k]
     if dwk:
         F, L = 4 * E, cfg.n_layer
         shapes = [(Vp, E)] + [(F + 1, E), (E + 1, F), (E + 1, E), (E + 1, E), (E + 1, E), (E + 1, 3 * E)] * L + \
                  [(E + 1, 2 * E * L)]
-        alg = statistics.mean(2 * T * m + 2 * T * n + 4 * m * n for m, n in shapes)
         nd = sum(len(fetch[k]) for k in dwk)
+        # per launch: the class's algorithmic bytes per step over its launches per step (74 single launches,
+        # or fewer when pairs of them run as one grouped launch); steps = training forwards in the pass
+        steps = sum(len(v) for k, v in fetch.items() if "embed_sort_kernel" in k) or 1
+        alg = sum(2 * T * m + 2 * T * n + 4 * m * n for m, n in shapes) / (nd / steps)
         fb = 2.0 * sum(sum(fetch[k]) for k in dwk) / nd
         wb = sum(sum(write.get(k, [])) for k in dwk) / max(1, sum(len(write.get(k, [])) for k in dwk))
         res["dw_class"] = {"kernels": [k.split("(")[0] for k in dwk], "dispatches": nd, "fetch_bytes": fb,
                            "write_bytes": wb, "hbm_bytes": fb + wb, "algorithmic_bytes": alg,
                            "ratio": (fb + wb) / alg,
+                           "launches_per_step": nd / steps,
                            "note": "mean per launch over the class; algorithmic = X^T and dY bf16 read once + dW f32 "
-                                   "written once, mean over the step's 74 launches"}
+                                   "written once, summed over the step's 74 GEMMs / the class's launches per step"}
     ad = pick(lambda k: "adamw_kernel" in k)
     if ad:
         k, fb, wb = ad
