@@ -3,7 +3,9 @@ from the environment when each model's plan is created), the variants' steps run
 inside ONE process, so slow box drift (clock, thermals) hits every variant alike.
 
 Usage (GPU box): python tools/ab_inproc.py "label:ENV=v,ENV2=w:defer" "label2::" [--blocks 8] [--steps 10]
-  the third field holds comma-separated flags: defer (deferred block updates), nb=N (AdamW grid cap).  Prints the median ms/step per variant."""
+  the third field holds comma-separated flags: defer (deferred block updates), nb=N (AdamW grid cap),
+  ov=M/N/K/a_layout/b_layout/cfg/split (a GEMM configuration override, set before each of the variant's blocks;
+  same split as the automatic plan, so the scratch sized at plan creation fits).  Prints the median ms/step per variant."""
 import os
 import statistics
 import sys
@@ -66,9 +68,20 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-        variants.append((label, step, []))
+        ovs = [tuple(int(x) for x in f[3:].split("/")) for f in flags.split(",") if f.startswith("ov=")]
+        variants.append((label, step, [], ovs))
+    from ergm_amd import _lib as L
+    lib = L.load()
+    all_ov = {o[:5] for v in variants for o in v[3]}
+
+    def use(ovs):  # GEMM configuration overrides of one variant (cfg only: the plans' scratch is unchanged)
+        for key in all_ov:
+            L.check(lib.ergm_gemm_set_override(*key, -1, 1), "override reset")
+        for o in ovs:
+            L.check(lib.ergm_gemm_set_override(*o), "override")
     for _ in range(blocks):
-        for label, step, times in variants:
+        for label, step, times, ovs in variants:
+            use(ovs)
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -77,7 +90,7 @@ def main():
             torch.cuda.synchronize()
             times.append(1000.0 * (time.perf_counter() - t0) / nsteps)
     base = statistics.median(variants[0][2])
-    for label, _, times in variants:
+    for label, _, times, _ in variants:
         med = statistics.median(times)
         print(f"{label:12s} median {med:7.3f} ms/step  ({100.0 * (med / base - 1):+5.1f} %)  min {min(times):7.3f}  "
               f"all {' '.join(f'{t:.2f}' for t in times)}", flush=True)
