@@ -47,7 +47,9 @@ SHAPES = [
 ]
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
         (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
-        (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128)]
+        (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
+        (256, 256), (128, 128), (128, 128),                       # 22-24 LDS-free epilogue variants
+        (256, 256), (128, 128), (256, 128), (128, 128)]           # 25-28 32-deep stages
 REPS = 20
 
 
@@ -150,6 +152,8 @@ def main():
 
         row["times"]["auto"] = run_cfg(-1, 0)
         cfgs = range(len(CFGS)) if not quick else [0, 1, 3, 4, 7]
+        if "--cfgs" in sys.argv:  # an explicit list, e.g. --cfgs 2,6,25,26
+            cfgs = [int(c) for c in sys.argv[sys.argv.index("--cfgs") + 1].split(",")]
         if "--auto-only" in sys.argv:  # only the automatic plan of every shape (A/B of two builds)
             cfgs = []
         for cfg in cfgs:
