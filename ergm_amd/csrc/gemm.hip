@@ -323,17 +323,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 // Pipelined variant: NS-stage LDS ring filled by LDS-DMA (GldsTile, tiles.h), counted waits, raw barrier.
 // The body takes its workgroup index `bid` (the tile, before the XCD remap) so that a grouped launch can run
 // several problems in one grid (gemm_dw2_kernel).
-// BK: the K depth of one ring stage (64, or 32 for the large tiles: twice the stages in the same LDS, so
-// more of the operand stream is in flight per workgroup).
-template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
-          int BK = GEMM_BK>
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
 __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid) {
     constexpr int NW = WGM * WGN;
     constexpr int WM = BM / WGM, WN = BN / WGN;
     constexpr int FM = WM / 16, FN = WN / 16;
-    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+    constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
     constexpr int STAGE = A_BYTES + B_BYTES;
-    constexpr int LPS = GldsTile<BM, A_KM, NW, BK>::PER_WAVE + GldsTile<BN, B_KN, NW, BK>::PER_WAVE;  // vmcnt/stage
+    constexpr int LPS = GldsTile<BM, A_KM, NW>::PER_WAVE + GldsTile<BN, B_KN, NW>::PER_WAVE;  // vmcnt per stage
     static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -349,7 +346,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = zs * a.k_per_split;
     const int kend = min(a.K, kbeg + a.k_per_split);
-    const int nk = (kend - kbeg) / BK;
+    const int nk = (kend - kbeg) / GEMM_BK;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / WGN, wn = wave % WGN;
 
@@ -361,16 +358,16 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
 
     auto issue_stage = [&](int kt) {
         char* st = smem + (kt % NS) * STAGE;
-        const int k0 = kbeg + kt * BK;
-        GldsTile<BM, A_KM, NW, BK>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
-        GldsTile<BN, B_KN, NW, BK>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
+        const int k0 = kbeg + kt * GEMM_BK;
+        GldsTile<BM, A_KM, NW>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
+        GldsTile<BN, B_KN, NW>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue_stage(s);
 
-    FragReader<BM, A_KM, BK> la;
-    FragReader<BN, B_KN, BK> lb;
+    FragReader<BM, A_KM> la;
+    FragReader<BN, B_KN> lb;
     // weight-gradient bias: the waves of the last tile row with wm == 0 also sum the B (dY) fragments they
     // read: lane l holds B[k = 8(l>>4) .. +7][n = l & 15] of each 16-column fragment
     constexpr bool CS = A_KM && B_KN && EPI == ERGM_EPI_NONE && !OUT_BF16;
@@ -391,7 +388,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
             if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
             const char* st = smem + (kt % NS) * STAGE;
 #pragma unroll
-            for (int ks = 0; ks < BK / 32; ++ks) {
+            for (int ks = 0; ks < 2; ++ks) {
                 bf16x8 fa[FM], fb[FN];
 #pragma unroll
                 for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
@@ -454,10 +451,9 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
-          int BK = GEMM_BK>
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
-    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT, BK>(a, blockIdx.x);
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT>(a, blockIdx.x);
 }
 
 // Two weight-gradient GEMMs (KM x KN, f32 out, no split) in ONE launch: workgroups [0, b1) run problem 0
@@ -695,7 +691,6 @@ struct PipeCfg {
     int bm, bn, wgm, wgn, ns;
     int np = 0;      // > 0: warp-specialised kernel with np producer waves
     bool direct = false;  // LDS-free epilogue (store_tile_direct); split-K partials keep the staged one
-    int bk = GEMM_BK;     // K depth of one ring stage (32: twice the stages in the same LDS)
 };
 static constexpr PipeCfg kCfgs[] = {
     {64, 64, 2, 2, 4},     // 0
@@ -725,11 +720,6 @@ static constexpr PipeCfg kCfgs[] = {
     {256, 256, 4, 2, 2, 0, true},  // 22 the LM-head tile of cfg 6
     {128, 128, 4, 2, 2, 0, true},  // 23 cfg 10
     {128, 128, 2, 2, 2, 0, true},  // 24 cfg 2
-    // 32-deep stages: the large tiles with 3-5 stages in flight instead of 1-2
-    {256, 256, 4, 2, 4, 0, false, 32},  // 25 cfg 6's tile, 4 half-depth stages (128 KiB)
-    {128, 128, 2, 2, 6, 0, false, 32},  // 26 cfg 2's tile, 6 stages (96 KiB)
-    {256, 128, 4, 2, 6, 0, false, 32},  // 27 cfg 4's tile, 6 stages (144 KiB)
-    {128, 128, 4, 2, 6, 0, false, 32},  // 28 cfg 10's tile, 6 stages
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -897,7 +887,7 @@ template <int C, bool AKM, bool BKN, int EPI, bool OB>
 static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
     constexpr int nthreads = 64 * (c.wgm * c.wgn + c.np);
-    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * c.bk * 2,
+    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2,
                                     (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
     using KSplit = decltype(&gemm_pipe_kernel<16, 16, 1, 1, 2, AKM, BKN, ERGM_EPI_NONE, false>);
     KSplit k_split, k_full;
@@ -905,8 +895,8 @@ static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
         k_split = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
         k_full = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, EPI, OB>;
     } else {
-        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false, false, c.bk>;
-        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct, c.bk>;
+        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
+        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct>;
     }
     static bool attr = (hipFuncSetAttribute((const void*)k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         hipFuncSetAttribute((const void*)k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -944,11 +934,7 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 21: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
         case 22: launch_pipe_cfg<22, AKM, BKN, EPI, OB>(a, split, s); break;
         case 23: launch_pipe_cfg<23, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 24: launch_pipe_cfg<24, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 25: launch_pipe_cfg<25, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 26: launch_pipe_cfg<26, AKM, BKN, EPI, OB>(a, split, s); break;
-        case 27: launch_pipe_cfg<27, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<28, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<24, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 

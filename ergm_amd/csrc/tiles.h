@@ -18,19 +18,13 @@ __device__ __forceinline__ int swz_row(int row) { return row & 7; }  // 128-B ro
 __device__ __forceinline__ int swz_tr16(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }        // 256-B rows
 __device__ __forceinline__ int swz_tr8(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }  // 128-B rows
 
-// 32-deep stages (BK = 32: the pipelined kernel's half-depth ring for the large tiles, so that more stages fit
-// in LDS) keep the same images with 64-B k-contiguous rows: four chunks, swizzled c ^ 2·((row >> 2) & 1), which
-// spreads the 16 lanes of every ds_read_b128 lane group over the 16 four-bank slots.
-__device__ __forceinline__ int swz_row32(int row) { return ((row >> 2) & 1) << 1; }
-
-template <int ROWS, bool TRANS, int BK = GEMM_BK>
+template <int ROWS, bool TRANS>
 struct TileLoader {
-    // ROWS = tile extent along M (A) or N (B).  !TRANS: tile [ROWS][BK] (k contiguous);
-    // TRANS: tile [BK][ROWS] (ROWS contiguous).
-    static_assert(BK == 64 || BK == 32, "64- or 32-deep stages");
-    static constexpr int CHUNKS = ROWS * BK / 8;             // 16-B chunks per tile
+    // ROWS = tile extent along M (A) or N (B).  !TRANS: tile [ROWS][64] (k contiguous);
+    // TRANS: tile [64][ROWS] (ROWS contiguous).
+    static constexpr int CHUNKS = ROWS * GEMM_BK / 8;       // 16-B chunks per tile
     static constexpr int PER_THREAD = CHUNKS / GEMM_THREADS;
-    static constexpr int CPR = TRANS ? ROWS / 8 : BK / 8;    // chunks per LDS row
+    static constexpr int CPR = TRANS ? ROWS / 8 : 8;         // chunks per LDS row
     static constexpr int ROW_BYTES = CPR * 16;
     static_assert(PER_THREAD >= 1, "tile too small");
 
@@ -63,7 +57,7 @@ struct TileLoader {
             int c = threadIdx.x + i * GEMM_THREADS;
             int lrow = c / CPR, lc = c % CPR;
             int pc;
-            if (!TRANS) pc = lc ^ (BK == 64 ? swz_row(lrow) : swz_row32(lrow));
+            if (!TRANS) pc = lc ^ swz_row(lrow);
             else pc = lc ^ (CPR == 16 ? swz_tr16(lrow) : swz_tr8(lrow));
             *reinterpret_cast<uint4*>(lds + lrow * ROW_BYTES + pc * 16) = regs[i];
         }
@@ -75,8 +69,7 @@ struct TileLoader {
         if (!TRANS) {
             int row = ro + (lane & 15);
             int ch = ks * 4 + (lane >> 4);
-            const int sw = BK == 64 ? swz_row(row) : swz_row32(row);
-            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ sw) << 4));
+            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ swz_row(row)) << 4));
         } else {
             int i16 = lane & 15, g = lane >> 4;
             int k = ks * 32 + 8 * g + (i16 >> 2);
@@ -148,11 +141,11 @@ __device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int ROWS, bool TRANS, int NWAVES, int BK = GEMM_BK>
+template <int ROWS, bool TRANS, int NWAVES>
 struct GldsTile {
-    static constexpr int BYTES = ROWS * BK * 2;
+    static constexpr int BYTES = ROWS * GEMM_BK * 2;
     static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;   // wave-instructions per wave per stage
-    static constexpr int CPR = TRANS ? ROWS / 8 : BK / 8;
+    static constexpr int CPR = TRANS ? ROWS / 8 : 8;
     static constexpr int ROW_BYTES = CPR * 16;
     static_assert(PER_WAVE >= 1 && PER_WAVE * 1024 * NWAVES == BYTES, "tile / wave count mismatch");
 
@@ -167,7 +160,7 @@ struct GldsTile {
             const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
             const __bf16* src;
             if (!TRANS) {
-                const int c = pc ^ (BK == 64 ? swz_row(row) : swz_row32(row));
+                const int c = pc ^ swz_row(row);
                 const int r = min(r0 + row, Rlim - 1);
                 src = base + (size_t)r * ld + k0 + c * 8;
             } else {
@@ -181,7 +174,7 @@ struct GldsTile {
 };
 
 // Fragment reader for a staged tile (any wave count): same LDS image and swizzles as TileLoader.
-template <int ROWS, bool TRANS, int BK = GEMM_BK>
-using FragReader = TileLoader<ROWS, TRANS, BK>;
+template <int ROWS, bool TRANS>
+using FragReader = TileLoader<ROWS, TRANS>;
 
 }  // namespace ergm

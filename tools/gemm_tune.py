@@ -48,8 +48,7 @@ SHAPES = [
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
         (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
         (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
-        (256, 256), (128, 128), (128, 128),                       # 22-24 LDS-free epilogue variants
-        (256, 256), (128, 128), (256, 128), (128, 128)]           # 25-28 32-deep stages
+        (256, 256), (128, 128), (128, 128)]                       # 22-24 LDS-free epilogue variants
 REPS = 20
 
 
