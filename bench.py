@@ -429,8 +429,9 @@ def main():
         probe_flops = sum(flops) / len(flops)
         achieved = sum(flops) / (sum(durs) * 1e-3) / 1e12
         probe_name = (f"weight-gradient GEMM class (dW = X^T.dY, KM x KN operands, fp32 out; the step's largest "
-                      f"time class): {n_l} launches per step = every block's 6 Conv1D dW (bias gradient summed in the same GEMM), the "
-                      "stacked caption K/V dW and the tied LM-head dW; achieved = sum of their algorithmic FLOPs "
+                      f"time class): {n_l} launches per step for every block's 6 Conv1D dW (bias gradient summed in the same "
+                      "GEMM; pairs whose problems underfill the chip grouped into one launch), the stacked caption K/V dW and "
+                      "the tied LM-head dW; achieved = sum of their algorithmic FLOPs "
                       f"/ sum of their in-step launch durations (HIP events around each launch, {n_probe_steps} steps run "
                       "right after the timed region)")
         traffic, traffic_src = pmc_traffic("dw_class", args.config)
