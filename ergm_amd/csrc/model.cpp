@@ -128,6 +128,7 @@ struct ergm_model_plan {
     int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
     bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
     bool dw_group;  // ... and a qualifying pair as ONE grouped launch (gemm_dw_pair)
+    int opt_lag = 2;  // ERGM_OPT_LAG: stages between a block's backward and its AdamW launch (opt_after_layer)
     std::vector<DwJob> dw_pend;
     bool bwd_forked;
     hipStream_t fwd2;
@@ -695,6 +696,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
     P->dw_group = true;
     if (const char* e = getenv("ERGM_DW_GROUP")) P->dw_group = atoi(e) != 0;
+    if (const char* e = getenv("ERGM_OPT_LAG")) P->opt_lag = std::max(0, atoi(e));
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -1433,17 +1435,24 @@ int opt_wte(ergm_model_plan* P, int select) {  // the tied wte's untouched (0) /
 int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
     if (!P->opt_on || P->dry) return ERGM_OK;
     const int L = P->d.n_layer, i = L - 1 - l;
-    if (i >= 1 && !P->opt.defer) {  // block l+1's gradients (bucket i-1) are final: this stage and its weight-gradient mark
-        ERGM_TRY(opt_wait(P, s, l + 1));
-        ERGM_TRY(opt_range(P, P->opt.ranges[2 * (i - 1)], P->opt.ranges[2 * (i - 1) + 1]));
+    // Block m's bucket (L-1-m) is final with its weight-gradient mark m (recorded after the LayerNorm reduce,
+    // which waited for the stage's last LayerNorm backward, so the stage has read the old weights).  Its AdamW
+    // is launched `lag` stages later (ERGM_OPT_LAG, default 2): the update then overlaps later blocks' backward
+    // instead of competing with its own block's weight-gradient GEMMs (bench A/B: lag 2 vs 1 C2 -0.4 %, C5
+    // -0.6 %, C4 equal; lag 0 slower).
+    const int lag = P->opt_lag;
+    auto upd = [&](int m) -> int {
+        ERGM_TRY(opt_wait(P, s, m));
+        return opt_range(P, P->opt.ranges[2 * (L - 1 - m)], P->opt.ranges[2 * (L - 1 - m) + 1]);
+    };
+    if (!P->opt.defer) {
+        if (l + lag <= L - 1) ERGM_TRY(upd(l + lag));
+        if (l == 0)  // the remaining blocks, last stage first
+            for (int m = std::min(lag, L) - 1; m >= 0; --m) ERGM_TRY(upd(m));
     }
-    if (i == 1) {  // the LM-head part of the tied wte is final after its weight-gradient GEMM (mark L+1)
+    if (i == std::min(1, L - 1) && !(L == 1 && lag >= 1)) {  // the LM-head part of the tied wte (mark L+1)
         ERGM_TRY(opt_wait(P, s, L + 1));
         ERGM_TRY(opt_wte(P, 0));
-    }
-    if (l == 0 && !P->opt.defer) {  // block 0 (bucket L-1): final with this stage's mark, not the embedding stage
-        ERGM_TRY(opt_wait(P, s, 0));
-        ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
     }
     return ERGM_OK;
 }
@@ -1452,7 +1461,7 @@ int opt_after_embed(ergm_model_plan* P, hipStream_t s) {
     const int L = P->d.n_layer;
     ERGM_TRY(opt_wait(P, s, -1));  // the embedding stage joined every side-stream gradient
     if (P->opt.defer) ERGM_TRY(opt_range(P, P->opt.ranges[2 * (L - 1)], P->opt.ranges[2 * (L - 1) + 1]));
-    if (L == 1) ERGM_TRY(opt_wte(P, 0));
+    if (L == 1 && P->opt_lag >= 1) ERGM_TRY(opt_wte(P, 0));
     ERGM_TRY(opt_range(P, P->opt.ranges[2 * L], P->opt.ranges[2 * L + 1]));
     ERGM_TRY(opt_wte(P, 1));
     hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
