@@ -1,6 +1,9 @@
 """In-process A/B of executor variants on the C2 step: one model per variant (plan-level switches are read
 from the environment when each model's plan is created), the variants' steps run in alternating blocks
 inside ONE process, so slow box drift (clock, thermals) hits every variant alike.
+CAVEAT: every model's executor creates its own streams and a process maps its streams onto 4 hardware queues,
+so from the third variant on streams of different models share queues and can serialise each other (~+20 %
+whatever the variant): compare two variants at a time, and confirm with sequential runs (tools/ab.sh).
 
 Usage (GPU box): python tools/ab_inproc.py "label:ENV=v,ENV2=w:defer" "label2::" [--blocks 8] [--steps 10]
   the third field holds comma-separated flags: defer (deferred block updates), nb=N (AdamW grid cap),

@@ -3,6 +3,8 @@ hardware queues — several models in one process share the process's 4 hardware
 other's streams, which made tools/ab_inproc.py's third and later variants ~20 % slow).  The controller lets the
 workers run blocks of steps in turn (never two at once), so slow box drift hits every variant alike.
 
+CAVEAT: the idle workers keep their hardware queues mapped, and beyond the firmware's queue slots the active
+worker is time-sliced against them (an identical second worker measured +4.4 %): prefer tools/ab.sh.
 Usage (GPU box): python tools/ab_procs.py "label:ENV=v,ENV2=w" "label2:" [--blocks 8] [--steps 10]
 Prints the median ms/step per variant."""
 import os
