@@ -5,12 +5,20 @@ MELD-shaped synthetic batches, GPT-2-small + audio/visual fusion, batch 16 per G
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--no-cpu-baseline]
 
 Prints ONE JSON line on rank 0.  ``value`` = all utterances processed by all ranks ÷ the max over
-ranks of the wall time of exactly K steps (barrier + device sync on both sides).  ``roofline`` is
-for the tied LM-head forward GEMM (the single largest GEMM launch of the step, a kernel symbol that
-nothing else in the step uses), timed with HIP events recorded by the native executor around that
-launch inside the timed steps; ``mfma_step`` is the whole step's algorithmic FLOPs
-over the step time against the 2.5 PF/s dense bf16 peak.  ``cpu_baseline`` times the CPU oracle
-(fp32 PyTorch restatement of the reference step) on the host cores for a bounded sample.
+ranks of the wall time of exactly K steps (barrier + device sync on both sides).  ``roofline`` is the
+step's dominant time class, the weight-gradient GEMMs (every Conv1D dW, the stacked caption K/V dW and
+the tied LM-head dW): their algorithmic FLOPs over their in-step launch durations, from HIP event
+pairs the native executor records around each launch in extra steps run right after the timed region
+(``--probe 1..4`` times a single launch inside the timed steps instead); ``roofline_secondary`` is the
+LM-head forward main launch; ``mfma_step`` is the whole step's algorithmic FLOPs over
+the step time against the 2.5 PF/s dense bf16 peak.  ``cpu_baseline`` times the CPU oracle (fp32
+PyTorch restatement of the reference step) on the host cores for a bounded sample.
+
+Reproducible: ``torch.manual_seed(--seed)`` before the model is built fixes the dropout mask stream
+(rank 0's seed is broadcast under DP), so two runs of a config print the same ``train_metrics``.
+Data parallel (N > 1): the bf16 gradient exchange with the sharded AdamW (ZeRO-1) unless
+ERGM_DP_GRAD / ERGM_DP_ZERO say otherwise (the library's defaults are the fp32 all-reduce and the
+replicated update).
 """
 from __future__ import annotations
 
@@ -182,7 +190,12 @@ def main():
                          "gpu_only_ms_per_step")
     ap.add_argument("--pdrop", type=float, default=None,
                     help="attn/resid/embd dropout (default: the config's 0.1, as the reference trains; 0 = off)")
+    ap.add_argument("--seed", type=int, default=0, help="torch.manual_seed before the model is built (dropout masks)")
     args = ap.parse_args()
+    # the bench's data-parallel exchange: bf16 with the sharded optimizer update (library defaults: fp32 all-reduce,
+    # replicated update; tests/test_dist_gloo.py bounds the bf16 trajectory against the fp32 one)
+    os.environ.setdefault("ERGM_DP_GRAD", "bf16")
+    os.environ.setdefault("ERGM_DP_ZERO", "1")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # self-launch: one fresh process per GPU, before anything here initialises HIP
@@ -249,6 +262,7 @@ def main():
     cfg = ERGMConfig(**MODELS[mname], feat_dim=Fd, fp8=fp8)
     if args.pdrop is not None:
         cfg.attn_pdrop = cfg.resid_pdrop = cfg.embd_pdrop = args.pdrop
+    torch.manual_seed(args.seed)  # the dropout mask stream (GPT2LMHeadModel draws its seed from torch's generator)
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim,

@@ -653,8 +653,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     ERGM_CHECK_ARG(d.batch > 0 && d.seq >= 2 && d.seq <= d.n_positions, "model_create: bad batch/seq");
     ERGM_CHECK_ARG(d.n_layer > 0, "model_create: n_layer must be > 0");
     ERGM_CHECK_ARG(d.feat_dim >= 0 && d.feat_dim % 64 == 0, "model_create: feat_dim must be a multiple of 64");
-    ERGM_CHECK_ARG(!d.fp8 || (d.n_embd % 128 == 0 && d.n_inner % 128 == 0 && params->capkv_w),
-                   "model_create: fp8 needs n_embd, n_inner multiples of 128 and the f32 caption K/V weight");
+    ERGM_CHECK_ARG(!d.fp8 || (d.n_embd % 128 == 0 && d.n_inner % 128 == 0),
+                   "model_create: fp8 needs n_embd, n_inner multiples of 128");
     if (d.has_features && d.feat_dim > 0 && d.feat_dim != d.n_embd) {
         const ergm_model_params& q = *params;
         ERGM_CHECK_ARG(q.vproj_w_b && q.vproj_b && q.aproj_w_b && q.aproj_b && q.g_vproj_w && q.g_aproj_w,
@@ -1117,7 +1117,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         }
         ERGM_TRY(side_mark(P, L));
         if (P->f8)
-            for (int l = 1; l < L; ++l) ERGM_TRY(quant_layer_weights(P, l, ss));
+            for (int l = 1; l < L; ++l) {
+                // a deferred AdamW update of block l (FusedAdamW(defer=True)) writes the bf16 shadow the
+                // quantiser reads: the side stream waits for it like block l's forward does
+                ERGM_TRY(wait_update(P, l, ss));
+                ERGM_TRY(quant_layer_weights(P, l, ss));
+            }
     }
     // Enqueue order: launch by launch, alternating chains (ERGM_FWD_INTERLEAVE=0: block by block).  The
     // forward's kernels are short, so the host's enqueue pace can set the GPU's: enqueued a block at a

@@ -12,20 +12,27 @@ data parallelism:
    stream as soon as the backward stage that finalises each bucket has been enqueued, so RCCL over
    xGMI overlaps the remaining backward.  The last bucket (caption K/V + wpe + wte) is final only after
    the embedding backward and cannot overlap.
-3. Exchange precision (``grad_comm``): "bf16" (default) moves bf16 gradients and accumulates in fp32 —
+3. Exchange precision (``grad_comm``): "fp32" (default) is a plain fp32 all-reduce — the reference's
+   gradient arithmetic (one fp32 sum per element, RCCL's order).  "bf16" (opt-in, ERGM_DP_GRAD=bf16; the
+   bench's choice) moves bf16 gradients and accumulates in fp32 —
    an all-to-all of bf16 chunks (rank r receives chunk r of every rank), an fp32 sum of the world
    copies of its chunk in rank order (ergm_chunk_sum_bf16, deterministic) rounded once to bf16, an
    all-gather of the reduced bf16 chunks, cast back into the fp32 gradient buffer: half the bytes of
    an fp32 all-reduce (2·(N−1)/N · 2 B per parameter), one rounding of the summed gradient, the same
-   result on every rank.  "fp32": a plain fp32 all-reduce.  ERGM_DP_GRAD selects (default bf16).
-4. Sharded optimizer (ZeRO-1, bf16 exchange with the overlapped FusedAdamW; ERGM_DP_ZERO=0 disables):
+   result on every rank.  Each rank's gradient is rounded to bf16 before the sum and the sum once more,
+   so the update differs from the fp32 exchange by about 2^-9 of each gradient element (bounded over
+   several steps by tests/test_dist_gloo.py).
+4. Sharded optimizer (ZeRO-1, opt-in: ERGM_DP_ZERO=1 with the bf16 exchange and the overlapped
+   FusedAdamW; the bench's choice):
    the all-to-all + chunk sum above IS a reduce-scatter, so rank r keeps the reduced gradient of its
    chunk only, applies AdamW to that chunk of the fp32 master, moments and bf16 shadow, and all-gathers
    the updated bf16 shadow chunks (the forward reads only the shadow).  Same bytes on the wire as the
    replicated exchange (2 + 2 B per parameter), 1/N of the AdamW pass (30 B/param of HBM traffic) per
    rank, and the same numbers: the update of every element is computed once, by its owner, from the
    same bf16-rounded reduced gradient.  Outside a rank's chunks the fp32 master, gradient and moments
-   are stale until ``consolidate_`` all-gathers them (checkpoints, a non-overlapped update).  The tied
+   are stale until ``consolidate_`` (a collective: every rank calls it) all-gathers them; until then
+   ``model.state_dict()`` and ``FusedAdamW.state_dict()`` raise instead of returning stale values
+   (the Trainer consolidates before each checkpoint; a non-overlapped update consolidates first).  The tied
    wte segment keeps the replicated update (its lookup rows are final only after the embedding
    backward and are exchanged as a compact block).
 
@@ -50,20 +57,23 @@ class DPSync:
         self._works: List = []
         self._stream = None
         self._events: List = []
-        self.grad_comm = grad_comm or os.environ.get("ERGM_DP_GRAD", "bf16")
+        self.grad_comm = grad_comm or os.environ.get("ERGM_DP_GRAD", "fp32")
         if self.grad_comm not in ("bf16", "fp32"):
             raise ValueError(f"grad_comm must be 'bf16' or 'fp32' (got {self.grad_comm!r})")
         self._pool = None          # bf16 exchange buffers, reused in stream order by every reduction
         self._pool32 = None        # fp32 gather buffer (consolidate_)
         self.bytes_per_step = 0    # gradient bytes this rank sent in the last backward (bench report)
-        self.zero = self.grad_comm == "bf16" and os.environ.get("ERGM_DP_ZERO", "1") != "0"
+        self.zero = self.grad_comm == "bf16" and os.environ.get("ERGM_DP_ZERO", "0") == "1"
         # consecutive block buckets exchanged together (ERGM_DP_MERGE, default 2): every exchange costs the
         # host ~0.15 ms of Python / ctypes / collective calls, which at 14 buckets per step left the host at
         # ~90 % of the GPU step under DP (bench ERGM_BENCH_FAKE_PG); two blocks per exchange halve that
         self.merge = max(1, int(os.environ.get("ERGM_DP_MERGE", "2")))
         self._pend_a: Optional[int] = None
-        # flat ranges [a, b) whose last update ran shard-wise (stale outside this rank's chunk)
+        # flat ranges [a, b) whose last update ran shard-wise: gradient and optimizer moments stale outside
+        # this rank's chunk (sharded), and the fp32 master too until a load_state_dict rewrites it
+        # (master_sharded)
         self.sharded: set = set()
+        self.master_sharded: set = set()
         self._master = None        # fp32 master whose directly-read elements stay replicated (set_master)
         self._mranges: List[Tuple[int, int]] = []
         self._midx: dict = {}
@@ -238,11 +248,13 @@ class DPSync:
             if self._master is not None:
                 self._sync_master(a, b, lo, hi)
             self.sharded.add((a, b))
+            self.master_sharded.add((a, b))
             return
         self.reduce_(grad[a:b])
         if post is not None:
             post(a, b)
         self.sharded.discard((a, b))
+        self.master_sharded.discard((a, b))
 
     def consolidate_(self, tensors, ranges=None) -> None:
         """All-gather the owners' chunks of every sharded range into each fp32 tensor (master, gradient,
@@ -255,6 +267,7 @@ class DPSync:
                 self.gather_(t[a:b], lo, hi)
         if ranges is None:
             self.sharded.clear()
+            self.master_sharded.clear()
 
     def _side(self, dev):
         if self._stream is None:

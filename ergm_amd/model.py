@@ -218,8 +218,17 @@ class GPT2LMHeadModel(nn.Module):
         self.process_group = process_group
         self._handle = id(self)
         _MODELS[self._handle] = self
-        # dropout mask stream: seed from torch's default generator, offset = training forwards so far
+        # dropout mask stream: seed from torch's default generator (torch.manual_seed makes it reproducible),
+        # offset = training forwards so far; under data parallelism rank 0's seed is broadcast so every rank
+        # draws the masks one process would draw for the concatenated batch (rows are global)
         self._drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if process_group is not None:
+            import torch.distributed as dist
+            if dist.get_world_size(process_group) > 1:
+                bdev = dev if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+                t = torch.tensor([self._drop_seed], dtype=torch.int64, device=bdev)
+                dist.broadcast(t, src=dist.get_global_rank(process_group, 0), group=process_group)
+                self._drop_seed = int(t.item())
         self._drop_offset = 0
         self.init_weights()
 
@@ -254,6 +263,10 @@ class GPT2LMHeadModel(nn.Module):
 
     def state_dict(self, *args, destination=None, prefix="", keep_vars=False):
         self.flush_deferred_()
+        if self.master_sharded:
+            raise RuntimeError("the sharded optimizer update (ZeRO-1, ERGM_DP_ZERO=1) left this rank's fp32 master "
+                               "valid only in its own chunks: call model.consolidate_() on EVERY rank (a collective) "
+                               "before state_dict()")
         out = OrderedDict() if destination is None else destination
         for name in state_dict_names(self.layout):
             src = "transformer.wte.weight" if name == "lm_head.weight" else name
@@ -277,8 +290,8 @@ class GPT2LMHeadModel(nn.Module):
         if "lm_head.weight" in state_dict and "transformer.wte.weight" not in state_dict:
             self.view("transformer.wte.weight").copy_(state_dict["lm_head.weight"])
         self.refresh_bf16()
-        for r in self._runners.values():  # every rank now holds the full master
-            r.dp.sharded.clear()
+        for r in self._runners.values():  # every rank now holds the full master (the moments stay sharded)
+            r.dp.master_sharded.clear()
         return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
 
     def flush_deferred_(self) -> None:
@@ -308,11 +321,18 @@ class GPT2LMHeadModel(nn.Module):
         rs[0].dp.consolidate_(ts, ranges)
         for r in rs:
             r.dp.sharded.clear()
+            r.dp.master_sharded.clear()
 
     @property
     def sharded(self) -> bool:
-        """True while some parameter range is only valid on its owner rank (see consolidate_)."""
+        """True while the gradient / optimizer moments of some parameter range are only valid on their owner
+        rank (see consolidate_)."""
         return any(r.dp.sharded for r in self._runners.values())
+
+    @property
+    def master_sharded(self) -> bool:
+        """True while the fp32 master of some parameter range is only valid on its owner rank."""
+        return any(r.dp.master_sharded for r in self._runners.values())
 
     @torch.no_grad()
     def refresh_bf16(self) -> None:

@@ -3,10 +3,11 @@
 ``FusedAdamW`` is a ``torch.optim.Optimizer`` with torch.optim.AdamW's hyper-parameters, defaults
 and state_dict format (``exp_avg``, ``exp_avg_sq``, ``step`` per parameter), so
 ``get_polynomial_decay_schedule_with_warmup`` (src/main.py:93-95) drives it unchanged.  Its one
-parameter is the model's flat fp32 buffer, so its optimizer checkpoints interchange with a
-``torch.optim.AdamW`` built over ``[model.flat]`` — not with the reference's per-tensor AdamW state
-(src/main.py:68,107), whose model part (the state_dict) does interchange.  ``step()`` is one HIP launch
-over the flat parameter buffer (``ergm_adamw_step``) that also refreshes the bf16 weight shadow.
+parameter is the model's flat fp32 buffer; ``reference_state_dict()`` / ``load_state_dict()`` convert
+to and from the reference's per-tensor ``torch.optim.AdamW`` state over ``model.parameters()``
+(src/main.py:68,107,188), so optimizer checkpoints interchange with the reference in both directions
+(tests/golden/optim_ref.npz).  ``step()`` is one HIP launch over the flat parameter buffer
+(``ergm_adamw_step``) that also refreshes the bf16 weight shadow.
 """
 from __future__ import annotations
 
@@ -15,6 +16,72 @@ import math
 import torch
 
 from . import ops
+
+# torch.optim.AdamW's per-group keys besides the hyper-parameters (a reference-format state dict carries them)
+_ADAMW_GROUP_DEFAULTS = {"amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                         "differentiable": False, "fused": None}
+
+
+def reference_param_names(layout):
+    """``model.parameters()`` order of the reference GPT2LMHeadModel (src/model.py:386-392,270-284,
+    599-608: wte, wpe, every block's ln_1, attn, ln_2, crossattention, ln_cross_attn, mlp, then ln_f and
+    emotion_head; the tied lm_head.weight is the wte Parameter and is yielded once) — the index order of
+    the reference optimizer's state (src/main.py:68).  Pinned by tests/golden/optim_ref.npz."""
+    from .params import state_dict_names
+    return [n for n in state_dict_names(layout) if n != "lm_head.weight"]
+
+
+def _view(layout, name: str, t: torch.Tensor) -> torch.Tensor:
+    v = layout.views[name]
+    return t.as_strided(v.shape, v.stride, v.offset)
+
+
+def reference_from_flat(layout, exp_avg, exp_avg_sq, step, group) -> dict:
+    """Flat AdamW state (moments laid out like the flat parameter buffer) -> the reference's per-tensor
+    ``torch.optim.AdamW`` state_dict over ``reference_param_names(layout)``."""
+    names = reference_param_names(layout)
+    state = {}
+    if exp_avg is not None:
+        stp = torch.as_tensor(step).detach().clone().float().cpu().reshape(())
+        for i, n in enumerate(names):
+            state[i] = {"step": stp.clone(), "exp_avg": _view(layout, n, exp_avg).detach().clone(),
+                        "exp_avg_sq": _view(layout, n, exp_avg_sq).detach().clone()}
+    g = {k: v for k, v in group.items() if k != "params"}
+    for k, v in _ADAMW_GROUP_DEFAULTS.items():
+        g.setdefault(k, v)
+    g["params"] = list(range(len(names)))
+    return {"state": state, "param_groups": [g]}
+
+
+def flat_from_reference(layout, state_dict, like: torch.Tensor):
+    """The reference's per-tensor AdamW state_dict -> (exp_avg, exp_avg_sq) flat tensors shaped like
+    ``like`` (padding zero), the common step, and the hyper-parameters of its group.  Raises ValueError
+    on a parameter count or shape that is not this layout's, or on per-parameter steps that differ."""
+    names = reference_param_names(layout)
+    grp = state_dict["param_groups"][0]
+    if len(grp["params"]) != len(names):
+        raise ValueError(f"optimizer state has {len(grp['params'])} parameters, the reference model.parameters() "
+                         f"of this configuration has {len(names)}")
+    m = torch.zeros_like(like)
+    v = torch.zeros_like(like)
+    steps = set()
+    ents = state_dict.get("state", {})
+    for i, pid in enumerate(grp["params"]):
+        e = ents.get(pid)
+        if not e:
+            continue
+        n = names[i]
+        dst = _view(layout, n, m)
+        if tuple(e["exp_avg"].shape) != tuple(dst.shape):
+            raise ValueError(f"optimizer state of {n}: shape {tuple(e['exp_avg'].shape)}, expected {tuple(dst.shape)}")
+        dst.copy_(e["exp_avg"])
+        _view(layout, n, v).copy_(e["exp_avg_sq"])
+        steps.add(float(e["step"]))
+    if len(steps) > 1:
+        raise ValueError(f"per-parameter AdamW steps differ ({sorted(steps)}): one flat step cannot hold them")
+    hp = {k: (tuple(grp[k]) if k == "betas" else grp[k]) for k in ("lr", "betas", "eps", "weight_decay", "initial_lr")
+          if k in grp}
+    return m, v, (steps.pop() if steps else 0.0), hp
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -121,9 +188,43 @@ class FusedAdamW(torch.optim.Optimizer):
         self._applied.add(id(flat))
         return d
 
+    # ---- checkpoint interchange with the reference's per-tensor torch.optim.AdamW state ----------------
+    def reference_state_dict(self) -> dict:
+        """The optimizer state in the reference's format (src/main.py:68,188): ``torch.optim.AdamW``
+        over ``model.parameters()`` of the reference GPT2LMHeadModel — one entry per parameter in that
+        order (the tied lm_head dropped), ``exp_avg`` / ``exp_avg_sq`` shaped like the parameter (wte
+        without its padding rows), ``step`` a float tensor.  ``torch.optim.AdamW(...).load_state_dict``
+        of the reference (and ``FusedAdamW.load_state_dict``) accept it."""
+        if self.model is None:
+            raise ValueError("reference_state_dict needs FusedAdamW(..., model=)")
+        self.state_dict()  # flushes deferred updates, refuses sharded moments
+        flat = self.model.flat
+        st = self.state.get(flat, {})
+        return reference_from_flat(self.model.layout, st.get("exp_avg"), st.get("exp_avg_sq"), st.get("step"),
+                                   self._group_of(flat))
+
+    def load_state_dict(self, state_dict):
+        """Either format: this optimizer's own (one flat parameter) or the reference's per-tensor
+        ``torch.optim.AdamW`` state over ``model.parameters()`` (a reference checkpoint's
+        ``optim_state_dict``), which is scattered into the flat moments through the layout views."""
+        groups = state_dict.get("param_groups", [])
+        flat = self.model.flat if self.model is not None else None
+        if flat is not None and len(groups) == 1 and len(groups[0]["params"]) != 1:
+            m, v, step, hp = flat_from_reference(self.model.layout, state_dict, flat.data)
+            grp = self._group_of(flat)
+            grp.update(hp)
+            self.state[flat] = {"step": torch.tensor(step), "exp_avg": m, "exp_avg_sq": v}
+            for r in self.model._runners.values():  # every rank now holds the full moments
+                r.dp.sharded.clear()
+            return
+        super().load_state_dict(state_dict)
+
     def state_dict(self):
         if self.model is not None:
             self.model.flush_deferred_()  # the moments of deferred block updates
+            if self.model.sharded:
+                raise RuntimeError("the sharded optimizer update (ZeRO-1) left this rank's AdamW moments valid only "
+                                   "in its own chunks: call model.consolidate_() on EVERY rank first")
         return super().state_dict()
 
     @torch.no_grad()

@@ -163,15 +163,14 @@ _SHADOW_ONLY = ("attn.c_attn.weight", "attn.c_proj.weight", "crossattention.q_at
 
 def master_read_ranges(layout: Layout, fp8: bool = False) -> List[Tuple[int, int]]:
     """Sorted, merged [start, end) element ranges of the fp32 master that the executor reads directly
-    (LayerNorm parameters, biases, wpe, the emotion head, the tied wte; with fp8 also the caption K/V
-    master, which the weight quantiser reads): everything except the Conv1D weight matrices, which it
-    reads through the bf16 shadow.  The sharded optimizer update (dist.py, ZeRO-1) keeps these
-    replicated in fp32 on every rank."""
+    (LayerNorm parameters, biases, wpe, the emotion head, the tied wte): everything except the Conv1D
+    weight matrices, which it reads through the bf16 shadow (the fp8 weight quantiser too, so ``fp8``
+    changes nothing).  The sharded optimizer update (dist.py, ZeRO-1) keeps these replicated in fp32 on
+    every rank."""
     skip = {f"transformer.h.{i}.{t}" for i in range(layout.L) for t in _SHADOW_ONLY}
     skip |= {"transformer.visual_proj.weight", "transformer.audio_proj.weight", "transformer.wte.weight"}
     skip |= {f"transformer.h.{i}.crossattention.c_attn.{t}" for i in range(layout.L) for t in ("weight", "bias")}
-    if not fp8:
-        skip.add("__capkv_w")
+    skip.add("__capkv_w")
     iv = sorted((v.offset, v.offset + v.numel) for k, v in layout.views.items() if k not in skip)
     out: List[Tuple[int, int]] = []
     for a, b in iv:

@@ -9,8 +9,10 @@ per epoch.  Validation (src/main.py:206-251) runs the inference forward under ``
 
 Checkpoints use the reference's keys (src/main.py:184-196: ``model_state_dict``, ``optim_state_dict``,
 ``sched_state_dict``, ``ppl``, ``epoch``) and file name pattern; the model's state_dict keys are the
-reference's, so the model part interchanges with reference checkpoints.  They are written with
-``torch.save`` and read back with ``torch.load(weights_only=True)``.
+reference's and the optimizer state is written in the reference's per-tensor AdamW format
+(``FusedAdamW.reference_state_dict``), so checkpoints interchange with the reference in both
+directions (``load`` accepts either optimizer format).  They are written with ``torch.save`` and read
+back with ``torch.load(weights_only=True)``.
 
 Data parallel: pass a ``process_group``; each rank iterates its own shard (e.g. a
 ``DistributedSampler``; every rank must run the same number of steps), the per-step losses are
@@ -129,8 +131,13 @@ class Trainer:
         return dist.get_rank(self.pg) == 0
 
     def state_dict(self) -> Dict:
+        # the optimizer part in the reference's per-tensor AdamW format when the optimizer can write it, so the
+        # reference's resume (src/main.py:107) loads this checkpoint and vice versa
+        ref_fmt = getattr(self.optim, "reference_state_dict", None)
+        optim_sd = ref_fmt() if ref_fmt is not None and getattr(self.optim, "model", None) is not None \
+            else self.optim.state_dict()
         return {"model_state_dict": {k: v.detach().clone() for k, v in self.model.state_dict().items()},
-                "optim_state_dict": self.optim.state_dict(),
+                "optim_state_dict": optim_sd,
                 "sched_state_dict": self.sched.state_dict() if self.sched is not None else None,
                 "ppl": self.best_ppl, "epoch": self.last_epoch}
 

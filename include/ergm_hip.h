@@ -320,7 +320,8 @@ typedef struct {
      * shadow), biases [E] f32, gradients f32; each bias stored right after its weight */
     const void* vproj_w_b; const float* vproj_b; const void* aproj_w_b; const float* aproj_b;
     float* g_vproj_w; float* g_vproj_b; float* g_aproj_w; float* g_aproj_b;
-    /* fp32 master of the stacked caption K/V weight [E][L*2E] (read by the fp8 weight quantiser) */
+    /* fp32 master of the stacked caption K/V weight [E][L*2E]; optional, not read by the executor (the
+     * fp8 weight quantiser reads the bf16 shadow capkv_w_b) */
     const float* capkv_w;
 } ergm_model_params;
 

@@ -377,6 +377,61 @@ def trainer_case(refmodel):
     return rec
 
 
+def optim_case(refmodel):
+    """The reference's optimizer state (src/main.py:68: ``torch.optim.AdamW(self.model.parameters())``,
+    saved / resumed as ``optim_state_dict`` at :107,188): parameter order of ``model.parameters()`` (the
+    tied lm_head dropped), the per-parameter ``exp_avg`` / ``exp_avg_sq`` / ``step`` after two reference
+    training steps, the step-3 gradient, and the parameters and state after the third ``optim.step()``."""
+    from transformers import GPT2Config
+    cfg = O.OracleConfig(vocab_size=128, n_embd=64, n_layer=1, n_head=1, n_positions=32)
+    seed = 77
+    P = O.init_params(cfg, seed=seed)
+    gcfg = GPT2Config(vocab_size=cfg.vocab_size, n_embd=cfg.n_embd, n_layer=cfg.n_layer, n_head=cfg.n_head,
+                      n_positions=cfg.n_positions, attn_pdrop=0.0, resid_pdrop=0.0, embd_pdrop=0.0)
+    net = refmodel.GPT2LMHeadModel(gcfg)
+    sd = dict(P)
+    sd["lm_head.weight"] = P["transformer.wte.weight"]
+    net.load_state_dict(sd, strict=True)
+    lr = 1e-3
+    optim = torch.optim.AdamW(net.parameters(), lr=lr)
+    names = {id(p): n for n, p in net.named_parameters()}
+    order = [names[id(p)] for p in optim.param_groups[0]["params"]]
+    batches = [synthetic_batch(4, 16, n_turns=2, feat_dim=cfg.n_embd, seed=seed + k, vocab_hi=125, sp1=126, sp2=127,
+                               eos=124) for k in range(3)]
+    net.train()
+    rec = {"config": np.array([cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_positions]),
+           "seed": np.array(seed), "lr": np.array(lr),
+           "param_order_json": np.frombuffer(json.dumps(order).encode(), dtype=np.uint8)}
+    for k, b in enumerate(batches):
+        out = net(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], labels=b["labels"],
+                  emotion_labels=b["emotion_labels"], caption_ids=b["caption_ids"], imgs=b["visual_feat"],
+                  auds=b["audio_feat"])
+        optim.zero_grad()
+        out.loss.backward()
+        if k == 2:  # before the third step: the resumable state, the parameters and the gradient
+            st = optim.state_dict()
+            for i, n in enumerate(order):
+                s = st["state"][i]
+                rec[f"st2:{n}:exp_avg"] = s["exp_avg"].numpy().copy()
+                rec[f"st2:{n}:exp_avg_sq"] = s["exp_avg_sq"].numpy().copy()
+                rec[f"st2:{n}:step"] = np.array(float(s["step"]))
+            for n, p in net.named_parameters():
+                rec[f"p2:{n}"] = p.detach().numpy().copy()
+                rec[f"g3:{n}"] = p.grad.detach().numpy().copy()
+        optim.step()
+    st = optim.state_dict()
+    for i, n in enumerate(order):
+        rec[f"st3:{n}:exp_avg"] = st["state"][i]["exp_avg"].numpy().copy()
+        rec[f"st3:{n}:exp_avg_sq"] = st["state"][i]["exp_avg_sq"].numpy().copy()
+    for n, p in net.named_parameters():
+        rec[f"p3:{n}"] = p.detach().numpy().copy()
+    g = st["param_groups"][0]
+    rec["group_json"] = np.frombuffer(json.dumps({k: v for k, v in g.items() if k != "params"}).encode(),
+                                      dtype=np.uint8)
+    print(f"  reference AdamW over {len(order)} parameters, state after 3 steps recorded")
+    return rec
+
+
 def main():
     torch.manual_seed(0)
     refmodel = load_reference()
@@ -385,7 +440,8 @@ def main():
         only = sys.argv[sys.argv.index("--only") + 1].split(",")
         cases = {"imgs2d": ("imgs2d_e64.npz", lambda: imgs2d_case(refmodel)),
                  "dataset": ("dataset_ref.npz", dataset_case),
-                 "trainer": ("trainer_ref.npz", lambda: trainer_case(refmodel))}
+                 "trainer": ("trainer_ref.npz", lambda: trainer_case(refmodel)),
+                 "optim": ("optim_ref.npz", lambda: optim_case(refmodel))}
         for c in only:
             fn, make = cases[c]
             np.savez_compressed(os.path.join(out_dir, fn), **make())
@@ -413,6 +469,8 @@ def main():
     np.savez_compressed(os.path.join(out_dir, "imgs2d_e64.npz"), **imgs2d_case(refmodel))
     np.savez_compressed(os.path.join(out_dir, "dataset_ref.npz"), **dataset_case())
     np.savez_compressed(os.path.join(out_dir, "trainer_ref.npz"), **trainer_case(refmodel))
+    # 8. the reference optimizer's per-parameter state (checkpoint interchange)
+    np.savez_compressed(os.path.join(out_dir, "optim_ref.npz"), **optim_case(refmodel))
     print("golden fixtures written to", out_dir)
 
 

@@ -176,3 +176,68 @@ def test_zero1_sharded_update_matches_replicated(world, merge):
     assert r["ok"]
     want = [(0, 1000), (1000, 2000), (2000, 4064)] if merge == 1 else [(0, 2000), (2000, 4064)]
     assert r["sharded"] == want and r["none"] == []
+
+
+def _traj_worker(rank, world, port, out_path, steps=5):
+    """The same DP training trajectory with the fp32 all-reduce (the default) and the bf16 exchange
+    (ERGM_DP_GRAD=bf16, the bench's choice): oracle gradients normalised by the global counts, the
+    exchange under test, the oracle's torch-AdamW update — losses and parameters per mode."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    layout = build_layout(CFG.vocab_size, CFG.n_embd, CFG.n_layer, CFG.inner, CFG.n_positions)
+    res = {}
+    for mode in ("fp32", "bf16"):
+        P = O.init_params(CFG, seed=4)
+        st = O.AdamWState()
+        dp = DPSync(dist.group.WORLD, dp_buckets(layout), grad_comm=mode)
+        losses = []
+        for it in range(steps):
+            full = synthetic_batch(B, S, n_turns=3, feat_dim=CFG.n_embd, seed=30 + it, vocab_hi=250, sp1=254,
+                                   sp2=255, eos=249)
+            lo, hi = rank * B // world, (rank + 1) * B // world
+            local = {k: v[lo:hi].clone() for k, v in full.items()}
+            n = torch.tensor([int((local["labels"][:, 1:] != -100).sum()), int((local["emotion_labels"] != -100).sum())],
+                             dtype=torch.int32)
+            n_local, e_local = n.tolist()
+            dp.reduce_count(n)
+            n_global, e_global = n.tolist()
+            leaves = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+            out = O.forward(leaves, CFG, **local)
+            loss = out["loss_lm"] * (n_local / n_global) + out["loss_emotion"] * (e_local / e_global)
+            loss.backward()
+            lt = loss.detach().clone()
+            dist.all_reduce(lt)
+            losses.append(lt.item())
+            grad = _flat_grads(layout, {k: v.grad for k, v in leaves.items()})
+            dp.begin()
+            for k in range(len(dp.buckets)):
+                dp.bucket_ready(k, grad)
+            dp.finish(grad)
+            g = {k: grad.as_strided(layout.views[k].shape, layout.views[k].stride, layout.views[k].offset).clone()
+                 for k in P}
+            O.adamw_step(P, g, st, 1e-3)
+        res[mode] = (losses, _flat_grads(layout, P))
+    if rank == 0:
+        torch.save({"fp32": res["fp32"], "bf16": res["bf16"], "p0": _flat_grads(layout, O.init_params(CFG, seed=4))},
+                   out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bf16_exchange_trajectory_stays_within_bound_of_fp32():
+    """the bf16 gradient exchange rounds each rank's gradient and the sum to bf16 (the
+    reference sums fp32 gradients on one device).  Over five AdamW steps on two ranks the bf16 trajectory
+    stays within a bound of the fp32 all-reduce's: every loss within 1e-3 relative, and the parameters'
+    distance within 2 % of the distance they travelled (AdamW's early updates are ~lr·sign(g): the bf16
+    rounding only flips the sign of gradient elements at the rounding level).  Measured here: loss 4.7e-5,
+    parameters 1.1e-2."""
+    path = os.path.join(tempfile.mkdtemp(), "t.pt")
+    mp.spawn(_traj_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    (l32, p32), (l16, p16) = r["fp32"], r["bf16"]
+    dl = max(abs(a - b) / abs(a) for a, b in zip(l32, l16))
+    dp = ((p16 - p32).norm() / (p32 - r["p0"]).norm()).item()
+    assert dl <= 1e-3 and dp <= 2e-2, (dl, dp)

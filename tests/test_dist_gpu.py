@@ -62,7 +62,16 @@ def _worker(rank, world, port, out_path, mode="fp32"):
     opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
     g = _step(model, opt, local, dev)
     res = {"sharded": model.sharded}
+    refused = []
+    for fn in (model.state_dict, opt.state_dict):
+        try:
+            fn()
+            refused.append(False)
+        except RuntimeError:
+            refused.append(True)
+    res["refused"] = refused
     model.consolidate_()  # sharded update (ZeRO-1): gather master, gradient and moments
+    res["sd_ok"] = len(model.state_dict()) > 0 and len(opt.state_dict()["state"]) == 1
     torch.cuda.synchronize()
     st = opt.state[model.flat]
     res.update(grad=model.flat.grad.clone().cpu(), flat=model.flat.detach().cpu(), m=st["exp_avg"].cpu(),
@@ -97,12 +106,15 @@ _RUNS = {}
 
 @pytest.mark.parametrize("mode", ["fp32", "bf16nz", "bf16"])
 def test_dp2_fused_step_matches_single_process(gpu, mode):
-    """Exchange precisions: "fp32" all-reduce; "bf16nz" the bf16 all-to-all / fp32 chunk sum /
-    all-gather (ergm_chunk_sum_bf16, ergm_cast_f32) with the replicated update; "bf16" (the default) the
-    same exchange with the sharded update (ZeRO-1) — bitwise the replicated one after consolidate_."""
+    """Exchange precisions: "fp32" all-reduce (the default); "bf16nz" the bf16 all-to-all / fp32 chunk sum /
+    all-gather (ergm_chunk_sum_bf16, ergm_cast_f32) with the replicated update; "bf16" the same exchange with
+    the sharded update (ZeRO-1, opt-in, the bench's choice) — bitwise the replicated one after consolidate_,
+    and until then model.state_dict() / FusedAdamW.state_dict() refuse (a rank-0 checkpoint
+    would mix trained and untrained chunks)."""
     torch.cuda.synchronize()
     r, r1 = _RUNS[mode] = _run(mode)
     assert r["sharded"] == (mode == "bf16") and r1["sharded"] == (mode == "bf16")
+    assert r["refused"] == [mode == "bf16"] * 2 and r1["refused"] == [mode == "bf16"] * 2 and r["sd_ok"]
     if mode == "bf16" and "bf16nz" in _RUNS:
         z = _RUNS["bf16nz"][0]
         for k in ("grad", "flat", "m", "v", "shadow"):
@@ -125,7 +137,7 @@ def _worker_dropout_trainer(rank, world, port, out_path):
     them)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["ERGM_DP_GRAD"] = "bf16"  # the default exchange
+    os.environ["ERGM_DP_GRAD"] = "bf16"  # the bench's exchange (replicated update: ZeRO-1 is opt-in)
     import torch.distributed as dist
     from ergm_amd.config import ERGMConfig
     from ergm_amd.model import GPT2LMHeadModel

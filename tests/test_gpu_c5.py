@@ -120,6 +120,43 @@ def test_fp8_full_depth_c5_geometry_matches_oracle(gpu):
     _grad_gate(_grads(model), og, rtol=FP8_GRAD_RTOL)
 
 
+def test_c5_bench_batch_equals_four_quarter_batches(gpu):
+    """The bench's own C5 shape (B=32, T=4096 tokens: the M=4096 GEMM plans, two forward chains of 16
+    samples) by a property the CPU oracle need not run for: with every sample carrying the same number of
+    valid LM labels and an emotion label, the B=32 loss is the mean of the four B=8 losses over the same
+    samples and its gradient the mean of their gradients (each B=8 step is itself held to the oracle by
+    test_fp8_full_depth_c5_geometry_matches_oracle).  Dropout off, fp8 forward as the bench runs it."""
+    V, E, Lyr, H, Fd = 50260, 1024, 24, 16, 768
+    _, cfg, P0 = _pair(V, E, Lyr, H, Fd, seed=26)
+    cfg.fp8 = True
+    model = GPT2LMHeadModel(cfg, device=gpu)
+    model.load_state_dict(P0, strict=True)
+    batch = synthetic_batch(32, 128, n_turns=5, feat_dim=Fd, seed=10)
+    lab = batch["input_ids"].clone()
+    lab[:, :64] = -100  # 64 valid shifted labels in every sample: equal normalisers per quarter
+    batch["labels"] = lab
+    out = _run(model, batch, gpu)
+    loss32, emo32 = out.loss.item(), out.emotion_logits.float().cpu()
+    g32 = model.flat.grad.detach().clone()
+    losses, gsum, emos = [], torch.zeros_like(g32), []
+    for k in range(4):
+        part = {n: v[8 * k:8 * (k + 1)] for n, v in batch.items()}
+        o = _run(model, part, gpu)
+        losses.append(o.loss.item())
+        emos.append(o.emotion_logits.float().cpu())
+        gsum += model.flat.grad
+    g8 = gsum / 4
+    assert abs(loss32 - sum(losses) / 4) <= 1e-4 * abs(loss32), (loss32, losses)
+    assert (emo32 - torch.cat(emos)).abs().max().item() <= 1e-3
+    names = [k for k in model.state_dict() if k != "lm_head.weight"]
+    bad = []
+    for n in names:
+        a, b = model.view(n, g32).double(), model.view(n, g8).double()
+        if (a - b).norm().item() > 3e-2 * max(b.norm().item(), 1e-12):
+            bad.append((n, ((a - b).norm() / b.norm().clamp_min(1e-30)).item()))
+    assert not bad, bad
+
+
 def test_fp8_weights_follow_the_optimizer(gpu):
     """The fp8 weight copies are re-quantised at every forward: after optimizer steps the trained fp8
     model's forward is bit-identical to that of a fresh fp8 model loaded with the updated weights, and
