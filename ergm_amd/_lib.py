@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 4  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 5  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -43,8 +43,8 @@ class GemmDesc(C.Structure):
 class AdamWDesc(C.Structure):
     _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
                 ("param_bf16", C.c_void_p), ("ranges", C.POINTER(C.c_int64)), ("n_ranges", C.c_int),
-                ("wte_begin", C.c_int64), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
-                ("eps", C.c_float), ("weight_decay", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float),
+                ("wte_begin", C.c_int64), ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
+                ("weight_decay", C.c_double), ("eps", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float),
                 ("max_blocks", C.c_int), ("defer", C.c_int)]
 
 
@@ -68,7 +68,7 @@ class ModelParams(C.Structure):
                 ("g_aproj_w", C.c_void_p), ("g_aproj_b", C.c_void_p), ("capkv_w", C.c_void_p)]
 
 
-vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
+vp, i32, i64, f32, f64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_double, C.c_size_t
 _SIGS = {
     "ergm_version": (i32, []),
     "ergm_last_error": (i32, [C.c_char_p, sz]),
@@ -99,8 +99,8 @@ _SIGS = {
     "ergm_xent_fwd_bwd": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
     "ergm_emotion_head": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     "ergm_loss_finalize": (i32, [vp, i32, vp, vp, vp, vp, vp]),
-    "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
-    "ergm_adamw_rows": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, i32, f32, f32, f32, f32, f32, f32, f32, i32, vp]),
+    "ergm_adamw_step": (i32, [vp, vp, vp, vp, vp, sz, f64, f64, f64, f32, f64, f32, f32, i32, vp]),
+    "ergm_adamw_rows": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, i32, f64, f64, f64, f32, f64, f32, f32, i32, vp]),
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
     "ergm_axpy": (i32, [vp, vp, sz, f32, vp]),
     "ergm_chunk_sum_bf16": (i32, [vp, i32, sz, vp, vp]),
@@ -125,6 +125,7 @@ _SIGS = {
     "ergm_model_backward_embed": (i32, [vp, vp]),
     "ergm_model_set_side_joins": (i32, [vp, i32]),
     "ergm_model_set_metrics": (i32, [vp, vp, vp]),
+    "ergm_model_set_logits_grad": (i32, [vp, vp]),
     "ergm_model_stage_wait": (i32, [vp, i32, vp]),
 }
 EXPORTED = sorted(_SIGS)

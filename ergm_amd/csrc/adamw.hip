@@ -148,8 +148,8 @@ static unsigned grid_for2(size_t n4) {  // adamw: each thread covers two strided
 
 using namespace ergm;
 
-extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
-                               float beta1, float beta2, float eps, float weight_decay, float step_size,
+extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, double lr,
+                               double beta1, double beta2, float eps, double weight_decay, float step_size,
                                float bc2_sqrt, int max_blocks, void* stream) {
     if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v, "adamw: null argument");
@@ -160,9 +160,9 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
     // the scalar products torch forms in double and rounds once when applied to fp32 tensors
-    float decay = (float)(1.0 - (double)lr * (double)weight_decay);
-    float one_m_b1 = (float)(1.0 - (double)beta1);
-    float one_m_b2 = (float)(1.0 - (double)beta2);
+    float decay = (float)(1.0 - lr * weight_decay);
+    float one_m_b1 = (float)(1.0 - beta1);
+    float one_m_b2 = (float)(1.0 - beta2);
     unsigned grid = grid_for2(n4);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
     // non-temporal parameter / moment traffic: C2 +1.2 %, C5 +0.6 % (profiles/r01_overlap_experiments.txt
@@ -170,18 +170,18 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     static const bool nt = !getenv("ERGM_ADAMW_NT") || atoi(getenv("ERGM_ADAMW_NT")) != 0;
     if (nt)
         hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
-                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2,
+                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
                            one_m_b2, eps, step_size, bc2_sqrt);
     else
         hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
-                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, beta2,
+                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
                            one_m_b2, eps, step_size, bc2_sqrt);
     return check_launch("adamw");
 }
 
 extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
-                               const void* row_flag, int select, float lr, float beta1, float beta2, float eps,
-                               float weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
+                               const void* row_flag, int select, double lr, double beta1, double beta2, float eps,
+                               double weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
     if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v && row_flag, "adamw_rows: null argument");
     ERGM_CHECK_ARG(rows >= 0 && row_len > 0 && row_len % 4 == 0, "adamw_rows: row_len must be a positive multiple of 4");
@@ -189,14 +189,14 @@ extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, voi
     ERGM_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), "adamw_rows: 16-byte alignment");
     ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw_rows: bf16 copy alignment");
     if (rows == 0) return ERGM_OK;
-    float decay = (float)(1.0 - (double)lr * (double)weight_decay);
-    float one_m_b1 = (float)(1.0 - (double)beta1);
-    float one_m_b2 = (float)(1.0 - (double)beta2);
+    float decay = (float)(1.0 - lr * weight_decay);
+    float one_m_b1 = (float)(1.0 - beta1);
+    float one_m_b2 = (float)(1.0 - beta2);
     unsigned grid = (unsigned)std::min(rows, 8192);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
     hipLaunchKernelGGL(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, rows, row_len / 4, (const uint8_t*)row_flag, select,
-                       decay, one_m_b1, beta2, one_m_b2, eps, step_size, bc2_sqrt);
+                       decay, one_m_b1, (float)beta2, one_m_b2, eps, step_size, bc2_sqrt);
     return check_launch("adamw_rows");
 }
 

@@ -323,7 +323,11 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 // Pipelined variant: NS-stage LDS ring filled by LDS-DMA (GldsTile, tiles.h), counted waits, raw barrier.
 // The body takes its workgroup index `bid` (the tile, before the XCD remap) so that a grouped launch can run
 // several problems in one grid (gemm_dw2_kernel).
-template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
+// IL = 1: the next stage's DMA pieces are issued between this step's fragment reads and MFMAs (half after the
+// first K half's reads, half after the second's) instead of all of them right after the barrier, so the wave's
+// LDS reads are in flight while the pieces queue at the texture unit and the fill overlaps the MFMAs.
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
+          int IL = 0>
 __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid) {
     constexpr int NW = WGM * WGN;
     constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -362,6 +366,13 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
         GldsTile<BM, A_KM, NW>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
         GldsTile<BN, B_KN, NW>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
     };
+    constexpr int PA = GldsTile<BM, A_KM, NW>::PER_WAVE;
+    auto issue_piece = [&](int kt, int p) {  // piece p of this wave's LPS pieces of stage kt (A's first)
+        char* st = smem + (kt % NS) * STAGE;
+        const int k0 = kbeg + kt * GEMM_BK;
+        if (p < PA) GldsTile<BM, A_KM, NW>::issue_piece(st, a.A, a.lda, m0, a.M, k0, wave, p);
+        else GldsTile<BN, B_KN, NW>::issue_piece(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave, p - PA);
+    };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue_stage(s);
@@ -385,7 +396,8 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
             wait_stages<LPS, NS - 2>(after);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot to refill are done
             __builtin_amdgcn_s_barrier();
-            if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+            const bool refill = kt + NS - 1 < nk;
+            if (!IL && refill) issue_stage(kt + NS - 1);
             const char* st = smem + (kt % NS) * STAGE;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
@@ -394,6 +406,13 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
                 for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
 #pragma unroll
                 for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+                if constexpr (IL != 0) {
+                    constexpr int H = (LPS + 1) / 2;
+                    if (refill) {
+#pragma unroll
+                        for (int p = ks * H; p < (ks + 1) * H && p < LPS; ++p) issue_piece(kt + NS - 1, p);
+                    }
+                }
                 if constexpr (SUM) {  // packed bf16 dot products against ones: 4 v_dot2 per fragment
                     const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
@@ -451,9 +470,125 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false>
+// Intra-workgroup split-K (KS2): 2·WGM·WGN waves in two groups of WGM×WGN.  Each barrier interval consumes a
+// PAIR of 64-deep K steps — group 0 the first, group 1 the second, on the same output tile — and refills one pair
+// slot; every wave of the workgroup issues its share of the DMA pieces, so a tile has twice the issuers of the
+// 4-wave kernel (the LDS-DMA fill, not the MFMA, bounds these tiles: ~25 GB/s landing per issuing wave) and half
+// the serial K steps.  At the end group 1's accumulators go through LDS into group 0's (acc_even + acc_odd per
+// element, fixed order: deterministic), then the staged epilogue with all waves copying out.  An odd K-step count
+// ends with a half-empty pair whose second half re-loads the first half's K step (so every pair issues the same
+// number of pieces and the counted waits stay exact) and group 1 skips it.
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__device__ __forceinline__ void gemm_ks2_body(const GemmArgs& a, const int bid) {
+    constexpr int NW = WGM * WGN;  // waves per group
+    constexpr int NT = 2 * NW;     // waves per workgroup
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
+    constexpr int HALF = A_BYTES + B_BYTES;  // one 64-deep K step
+    constexpr int STAGE = 2 * HALF;          // a pair
+    constexpr int LPS = 2 * (GldsTile<BM, A_KM, NT>::PER_WAVE + GldsTile<BN, B_KN, NT>::PER_WAVE);
+    static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int zs = (int)blockIdx.z;
+    const int id = xcd_remap(bid, nwg);
+    if (id >= nwg) return;
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = zs * a.k_per_split;
+    const int kend = min(a.K, kbeg + a.k_per_split);
+    const int nk = (kend - kbeg) / GEMM_BK;
+    const int npair = (nk + 1) / 2;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = wave / NW, wv = wave % NW;
+    const int wm = wv / WGN, wn = wv % WGN;
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_pair = [&](int kp) {
+        char* st = smem + (kp % NS) * STAGE;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kt = min(2 * kp + h, nk - 1);  // the odd tail's second half re-loads the last step
+            const int k0 = kbeg + kt * GEMM_BK;
+            GldsTile<BM, A_KM, NT>::issue(st + h * HALF, a.A, a.lda, m0, a.M, k0, wave);
+            GldsTile<BN, B_KN, NT>::issue(st + h * HALF + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < npair) issue_pair(s);
+
+    FragReader<BM, A_KM> la;
+    FragReader<BN, B_KN> lb;
+    for (int kp = 0; kp < npair; ++kp) {
+        wait_stages<LPS, NS - 2>(min(NS - 2, npair - 1 - kp));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kp + NS - 1 < npair) issue_pair(kp + NS - 1);
+        if (2 * kp + grp < nk) {
+            const char* st = smem + (kp % NS) * STAGE + grp * HALF;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fa[FM], fb[FN];
+#pragma unroll
+                for (int i = 0; i < FM; ++i) fa[i] = la.frag(st, wm * WM + i * 16, ks);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) fb[j] = lb.frag(st + A_BYTES, wn * WN + j * 16, ks);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    // group 1's partial tile into group 0's through LDS ([fragment register][lane] floats: conflict-free)
+    const int lane = threadIdx.x & 63;
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if (grp == 1) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[(((wv * FM + i) * FN + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((wv * FM + i) * FN + j) * 4 + r) * 64 + lane];
+    }
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    float* slab = a.slab ? a.slab + (size_t)zs * a.M * a.N : nullptr;
+    // store_tile opens with a barrier (group 0's reads of `red` are done before the staging reuse); only the
+    // group-0 waves hold accumulators, every wave helps with the copy-out
+    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * NT>(a, smem, acc, m0, n0, alpha, slab);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16>
+__global__ __launch_bounds__(128 * WGM * WGN) void gemm_ks2_kernel(GemmArgs a) {
+    gemm_ks2_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16>(a, blockIdx.x);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
+          int IL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
-    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT>(a, blockIdx.x);
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT, IL>(a, blockIdx.x);
 }
 
 // Two weight-gradient GEMMs (KM x KN, f32 out, no split) in ONE launch: workgroups [0, b1) run problem 0
@@ -465,15 +600,13 @@ struct GemmArgs2 {
     GemmArgs a[2];
     int b1;
 };
-template <int BM, int BN, int WGM, int WGN, int NS>
+template <int BM, int BN, int WGM, int WGN, int NS, int IL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_dw2_kernel(GemmArgs2 g) {
     const int b = blockIdx.x;
-    if (b < g.b1) {
-        if (b >= g.a[0].tiles_m * g.a[0].tiles_n) return;
-        gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false>(g.a[0], b);
-    } else {
-        gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false>(g.a[1], b - g.b1);
-    }
+    const int pr = b < g.b1 ? 0 : 1;
+    const int bb = pr == 0 ? b : b - g.b1;
+    if (pr == 0 && b >= g.a[0].tiles_m * g.a[0].tiles_n) return;
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false, false, IL>(g.a[pr], bb);
 }
 
 // Warp-specialised variant: NP producer waves only issue the LDS-DMA fills, the WGM x WGN consumer
@@ -691,6 +824,8 @@ struct PipeCfg {
     int bm, bn, wgm, wgn, ns;
     int np = 0;      // > 0: warp-specialised kernel with np producer waves
     bool direct = false;  // LDS-free epilogue (store_tile_direct); split-K partials keep the staged one
+    int il = 0;      // 1: next-stage DMA pieces interleaved with the step's reads / MFMAs (gemm_pipe_body IL)
+    int ks = 1;      // 2: intra-workgroup split-K over two wave groups (gemm_ks2_body; ns counts K-step pairs)
 };
 static constexpr PipeCfg kCfgs[] = {
     {64, 64, 2, 2, 4},     // 0
@@ -720,6 +855,21 @@ static constexpr PipeCfg kCfgs[] = {
     {256, 256, 4, 2, 2, 0, true},  // 22 the LM-head tile of cfg 6
     {128, 128, 4, 2, 2, 0, true},  // 23 cfg 10
     {128, 128, 2, 2, 2, 0, true},  // 24 cfg 2
+    // interleaved DMA issue (IL) variants of the automatic plans' configurations
+    {64, 64, 2, 2, 4, 0, false, 1},     // 25 cfg 0
+    {128, 128, 2, 2, 2, 0, false, 1},   // 26 cfg 2
+    {128, 128, 2, 4, 3, 0, false, 1},   // 27 cfg 3
+    {256, 256, 4, 2, 2, 0, false, 1},   // 28 cfg 6
+    {64, 128, 2, 2, 4, 0, false, 1},    // 29 cfg 8
+    {128, 128, 4, 2, 2, 0, false, 1},   // 30 cfg 10
+    {128, 128, 2, 2, 4, 0, false, 1},   // 31 cfg 14
+    {128, 128, 2, 2, 3, 0, false, 1},   // 32 cfg 1
+    // intra-workgroup split-K (KS2, 8 waves as two K groups of 2x2; ns = K-step PAIRS in the ring)
+    {64, 64, 2, 2, 2, 0, false, 0, 2},    // 33  64 KB
+    {64, 64, 2, 2, 3, 0, false, 0, 2},    // 34  96 KB
+    {64, 128, 2, 2, 2, 0, false, 0, 2},   // 35  96 KB
+    {128, 64, 2, 2, 2, 0, false, 0, 2},   // 36  96 KB
+    {128, 128, 2, 2, 2, 0, false, 0, 2},  // 37 128 KB
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -886,17 +1036,20 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
 template <int C, bool AKM, bool BKN, int EPI, bool OB>
 static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
-    constexpr int nthreads = 64 * (c.wgm * c.wgn + c.np);
-    constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2,
+    constexpr int nthreads = 64 * (c.wgm * c.wgn * c.ks + c.np);
+    constexpr size_t lds = std::max((size_t)c.ns * c.ks * (c.bm + c.bn) * GEMM_BK * 2,
                                     (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
     using KSplit = decltype(&gemm_pipe_kernel<16, 16, 1, 1, 2, AKM, BKN, ERGM_EPI_NONE, false>);
     KSplit k_split, k_full;
-    if constexpr (c.np > 0) {
+    if constexpr (c.ks == 2) {
+        k_split = gemm_ks2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
+        k_full = gemm_ks2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB>;
+    } else if constexpr (c.np > 0) {
         k_split = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
         k_full = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, EPI, OB>;
     } else {
-        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
-        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct>;
+        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false, false, c.il>;
+        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct, c.il>;
     }
     static bool attr = (hipFuncSetAttribute((const void*)k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         hipFuncSetAttribute((const void*)k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -934,7 +1087,20 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 21: launch_pipe_cfg<21, AKM, BKN, EPI, OB>(a, split, s); break;
         case 22: launch_pipe_cfg<22, AKM, BKN, EPI, OB>(a, split, s); break;
         case 23: launch_pipe_cfg<23, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<24, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 24: launch_pipe_cfg<24, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 25: launch_pipe_cfg<25, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 26: launch_pipe_cfg<26, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 27: launch_pipe_cfg<27, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 28: launch_pipe_cfg<28, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 29: launch_pipe_cfg<29, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 30: launch_pipe_cfg<30, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 31: launch_pipe_cfg<31, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 32: launch_pipe_cfg<32, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 33: launch_pipe_cfg<33, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 34: launch_pipe_cfg<34, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 35: launch_pipe_cfg<35, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 36: launch_pipe_cfg<36, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<37, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 
@@ -1179,10 +1345,10 @@ static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B,
     a.nt_store = nt_env && ((d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
                             (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE));
     // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
-    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0;
+    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1;
     a.colsum = cs_in ? d->bias_grad : nullptr;
     a.colsum_part = nullptr;
-    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 ? 1 : 0;
+    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 ? 1 : 0;
     return a;
 }
 }  // namespace ergm
@@ -1271,7 +1437,7 @@ static void launch_dw2_cfg(const GemmArgs2& g, int nblocks, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
     static_assert(c.np == 0 && !c.direct, "grouped dW launch: pipelined kernels with the staged epilogue only");
     constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
-    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns>;
+    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il>;
     static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
     (void)attr;
     hipLaunchKernelGGL(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
@@ -1290,8 +1456,9 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
     }
     GemmPlan p[2] = {plan_gemm(d[0]), plan_gemm(d[1])};
     const int cfg = p[0].cfg;
-    if (cfg < 0 || cfg >= 16 || p[1].cfg != cfg || p[0].split != 1 || p[1].split != 1 || p[0].xcd || p[1].xcd ||
-        kCfgs[cfg].np != 0 || kCfgs[cfg].direct)
+    if (cfg < 0 || (cfg >= 16 && kCfgs[cfg].il == 0) || kCfgs[cfg].ks != 1 || p[1].cfg != cfg || p[0].split != 1 ||
+        p[1].split != 1 ||
+        p[0].xcd || p[1].xcd || kCfgs[cfg].np != 0 || kCfgs[cfg].direct)
         return ERGM_EUNSUPPORTED;
     // only pairs whose problems each leave CUs idle: grouping two chip-filling GEMMs measured slower (C5:
     // 264 + 288 tiles, step +1.2 %); C2's pairs (150 + 168, 156 + 156 tiles) gain 0.4 %
@@ -1322,7 +1489,15 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
         case 12: launch_dw2_cfg<12>(g, nb, s); break;
         case 13: launch_dw2_cfg<13>(g, nb, s); break;
         case 14: launch_dw2_cfg<14>(g, nb, s); break;
-        default: launch_dw2_cfg<15>(g, nb, s); break;
+        case 15: launch_dw2_cfg<15>(g, nb, s); break;
+        case 25: launch_dw2_cfg<25>(g, nb, s); break;
+        case 26: launch_dw2_cfg<26>(g, nb, s); break;
+        case 27: launch_dw2_cfg<27>(g, nb, s); break;
+        case 29: launch_dw2_cfg<29>(g, nb, s); break;
+        case 30: launch_dw2_cfg<30>(g, nb, s); break;
+        case 31: launch_dw2_cfg<31>(g, nb, s); break;
+        case 32: launch_dw2_cfg<32>(g, nb, s); break;
+        default: return ERGM_EUNSUPPORTED;
     }
     return check_launch("gemm_dw_pair");
 }

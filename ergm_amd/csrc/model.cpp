@@ -10,7 +10,8 @@
 // One C call launches a whole stage (no per-op Python/ctypes overhead); every buffer is caller-owned.
 // Design points: the cross-attention K/V projection of the caption embeddings — the same
 // tensor in every block (src/model.py:521) — runs as ONE GEMM for all L blocks with the stacked
-// weights [E][L·2E]; its backward is likewise one dX GEMM (contraction over L·2E) and one dW GEMM.
+// weights [E][L·2E]; its backward is split back per block (each block stage issues its slice's dW and
+// accumulates its dX into the caption gradient), so none of it waits for the embedding stage.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,7 +34,7 @@ int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop);
+                       const DropSite& drop, int drop_res);
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
@@ -43,6 +44,7 @@ int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_globa
                           const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s);
 int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const void* const B[2], void* const C[2],
                  void* stream, bool launch);
+int dlogits_add(void* dl, const void* g, const float* scale, size_t n, hipStream_t s);
 int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, const float* wte, const float* wpe,
                  const float* vis, int ld_vis, const float* aud, float* h0, void* cap, int ld_cap, int B, int S, int E,
                  int V, hipStream_t s, const DropSite& drop);
@@ -80,6 +82,7 @@ struct DwJob {
     int ldy;
     float* gW;
     float* gB;
+    int ldc;  // row stride of gW (N, or the stacked matrix's width for a column slice)
 };
 
 struct ergm_model_plan {
@@ -128,6 +131,7 @@ struct ergm_model_plan {
     int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
     bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
     bool dw_group;  // ... and a qualifying pair as ONE grouped launch (gemm_dw_pair)
+    int capkv_split = 1;  // ERGM_CAPKV_SPLIT: caption K/V gradients per block stage (1) or stacked at the end (0)
     int opt_lag = 2;  // ERGM_OPT_LAG: stages between a block's backward and its AdamW launch (opt_after_layer)
     std::vector<DwJob> dw_pend;
     bool bwd_forked;
@@ -170,6 +174,7 @@ struct ergm_model_plan {
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
     const float *vis, *aud;
     const int* n_valid;  // [0] valid LM labels, [1] valid emotion labels (global under DP)
+    const void* logits_grad = nullptr;  // ergm_model_set_logits_grad: caller's bf16 gradient on the logits (next backward)
     float* metric_loss = nullptr;       // ergm_model_set_metrics: [0] += loss, [1] += LM loss per training forward
     int64_t* metric_correct = nullptr;  // += emotion argmax hits per training forward
     bool have_fwd;
@@ -478,8 +483,8 @@ int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
     DiagClass dc(P, 0);
     Probe pr(P, 5, s, dw_flops(P, j));
     if (P->fused_bias)
-        return gemm(P, s, j.M + 1, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE);
-    return gemm(P, s, j.M, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.N, ERGM_F32, ERGM_EPI_NONE,
+        return gemm(P, s, j.M + 1, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.ldc, ERGM_F32, ERGM_EPI_NONE);
+    return gemm(P, s, j.M, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.ldc, ERGM_F32, ERGM_EPI_NONE,
                 nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, j.gB);
 }
 // Two pending weight-gradient GEMMs as ONE grouped launch (gemm_dw_pair) when they plan to the same unsplit
@@ -493,7 +498,7 @@ int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJ
     for (int i = 0; i < 2; ++i) {
         memset(&g[i], 0, sizeof(g[i]));
         g[i].M = P->fused_bias ? j[i]->M + 1 : j[i]->M;
-        g[i].N = j[i]->N; g[i].K = T; g[i].lda = j[i]->lda; g[i].ldb = j[i]->ldy; g[i].ldc = j[i]->N;
+        g[i].N = j[i]->N; g[i].K = T; g[i].lda = j[i]->lda; g[i].ldb = j[i]->ldy; g[i].ldc = j[i]->ldc;
         g[i].a_layout = ERGM_KM; g[i].b_layout = ERGM_KN; g[i].c_dtype = ERGM_F32; g[i].epilogue = ERGM_EPI_NONE;
         g[i].alpha = 1.0f;
         g[i].bias_grad = P->fused_bias ? nullptr : j[i]->gB;
@@ -507,10 +512,10 @@ int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJ
     return gemm_dw_pair(d, A, B, C, s, true);
 }
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
-            float* gW, float* gB, int kind = 0) {
+            float* gW, float* gB, int kind = 0, int ldc = 0) {
     const bool on_main = (P->dw_main & kind) && ch.n == 1;
     if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
-    const DwJob j{M, N, A, lda, dY, ldy, gW, gB};
+    const DwJob j{M, N, A, lda, dY, ldy, gW, gB, ldc ? ldc : N};
     if (!on_main && P->dw_batch && !P->dry) {  // launched by the next dw_flush, behind one fork
         P->dw_pend.push_back(j);
         return ERGM_OK;
@@ -546,10 +551,12 @@ int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* 
     float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
     const size_t o = (size_t)r0 * E, po = (size_t)(r0 / 8) * E;
     // dh_b feeds the residual branch that produced this residual-stream tensor (slot = its index):
-    // through that branch's dropout (slot 0, the embeddings: unused by any GEMM)
+    // through that branch's dropout.  Slot 0 (the embeddings) has no bf16 consumer: there the final dh
+    // itself goes through the embedding dropout (src/model.py:506), folded into this pass.
     const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
-    return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, dh_b + o, pg + po, pb + po, rows,
-                              E, s, drop_site_of(&dd, E));
+    const int fin = slot == 0;
+    return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
+                              pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin);
 }
 int ln_reduce_add(ergm_model_plan* P, int slot, float* dgamma, float* dbeta) {
     if (P->dry) return ERGM_OK;
@@ -699,6 +706,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->dw_group = d.n_embd < 1024;
     if (const char* e = getenv("ERGM_DW_GROUP")) P->dw_group = atoi(e) != 0;
     if (const char* e = getenv("ERGM_OPT_LAG")) P->opt_lag = std::max(0, atoi(e));
+    if (const char* e = getenv("ERGM_CAPKV_SPLIT")) P->capkv_split = atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -847,6 +855,13 @@ extern "C" int ergm_model_set_dropout(ergm_model_plan* P, float attn_p, float re
     P->drop_seed = seed;
     P->drop_offset = offset;
     P->b_base = batch_base;
+    return ERGM_OK;
+}
+
+extern "C" int ergm_model_set_logits_grad(ergm_model_plan* P, const void* grad_logits) {
+    ERGM_CHECK_ARG(P, "model_set_logits_grad: null plan");
+    ERGM_CHECK_ARG(!grad_logits || aligned16(grad_logits), "model_set_logits_grad: 16-byte alignment");
+    P->logits_grad = grad_logits;
     return ERGM_OK;
 }
 
@@ -1208,10 +1223,18 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     // gradient dwte = dlogitsᵀ · ln_f(h) on the side stream (joined before the embedding backward adds
     // the lookup gradients into the same buffer).
     DiagClass dc(P, 128);
+    // a caller's gradient on the returned logits (src/model.py:698 returns differentiable logits): added to the
+    // cross-entropy's dlogits, scaled by the loss gradient there, so the LM-head GEMMs run with alpha 1
+    const float* lm_scale = gscale;
+    if (P->logits_grad && !P->dry) {
+        ERGM_TRY(dlogits_add(P->dlogits, P->logits_grad, gscale, (size_t)T * Vp, s));
+        lm_scale = nullptr;
+    }
+    P->logits_grad = nullptr;
     {
         Probe pr(P, 2, s);
         ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
-                      nullptr, nullptr, 0, nullptr, 0, gscale));
+                      nullptr, nullptr, 0, nullptr, 0, lm_scale));
     }
     {
         ERGM_TRY(fork_side(P, s));
@@ -1219,7 +1242,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
         Probe pr(P, 3, ss);
         Probe pr5(P, 5, ss, 2.0 * Vp * E * T);
         if (!(diag_skip() & 1)) ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
-                      ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, gscale));
+                      ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, lm_scale));
         ERGM_TRY(side_mark(P, L + 1));
     }
     if (P->dry) return ERGM_OK;
@@ -1288,7 +1311,23 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
     }
     ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), 8));
-    ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
+    if (P->capkv_split) {
+        // this block's slice of the stacked caption K/V projection: its weight gradient (columns
+        // [2El, 2E(l+1)) of [g_capkv_w; g_capkv_b]) joins the block's side-stream dW work, and the caption
+        // gradient dcap accumulates dKV_l·W_lᵀ on the data-gradient chain(s), so neither is left for the
+        // embedding stage at the end of the backward
+        DiagClass dcx(P, 2048);
+        const ergm_model_params& p = P->p;
+        const size_t co = (size_t)l * 2 * E;
+        const __bf16* dkv = P->dry ? nullptr : P->dkv_all + co;
+        ERGM_TRY(dw_gemm(P, ch, E, 2 * E, P->cap, P->XE, dkv, L2E, P->dry ? nullptr : p.g_capkv_w + co,
+                         P->dry ? nullptr : p.g_capkv_b + co, 64, L2E));
+        for (int c = 0; c < ch.n; ++c)
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 2 * E, R(dkv, c, L2E), L2E, ERGM_MK,
+                          P->dry ? nullptr : reinterpret_cast<const __bf16*>(p.capkv_w_b) + co, L2E, ERGM_NK, R(P->dcap, c, E), E, ERGM_F32,
+                          l == L - 1 ? ERGM_EPI_NONE : ERGM_EPI_ACCUM));
+    }
+    ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q + caption K/V weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1336,11 +1375,8 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
             return fail(ERGM_EHIP, "model: backward chain join");
         P->bwd_forked = false;
     }
-    const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
-    if (!P->dry) {  // dh = gradient of the dropped embedding sum: through the embedding dropout (src/model.py:506)
-        const ergm_dropout de = resid_drop(P, 0, 0);
-        ERGM_TRY(dropout_apply_f32(drop_site_of(&de, E), P->dh, T, E, E, s));
-    }
+    // dh is already the gradient of the embedding sum: block 0's first LayerNorm backward took it through
+    // the embedding dropout (ln_bwd_rows, slot 0)
     if (P->proj) {
         // feature projections: the projected vectors got dh0 at positions 0 / 1; dW = featᵀ·d over the
         // (padded) batch with the bias row fused (side stream); no gradient flows to the features
@@ -1361,13 +1397,17 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
                 return fail(ERGM_EHIP, "model: memset");
         }
     }
-    // stacked caption K/V projection of all blocks: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main)
-    DiagClass dc(P, 2048);
-    ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
-    ERGM_TRY(dw_flush(P, one));
+    if (!P->capkv_split) {  // stacked: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main), one GEMM each
+        DiagClass dc(P, 2048);
+        const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
+        ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
+        ERGM_TRY(dw_flush(P, one));
+        ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
+                      ERGM_EPI_NONE));
+    }
+    // (split: the block stages issued them, dW per block on the side stream, dcap on the chains); mark the
+    // side stream's caption / projection work
     ERGM_TRY(side_mark(P, L + 2));
-    ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
-                  ERGM_EPI_NONE));
     if (P->dry) return ERGM_OK;
     // the LM-head dwte (side stream, marked L+1) is final before the lookup gradients are added to it;
     // the caption K/V weight gradient keeps running on the side stream meanwhile

@@ -97,7 +97,8 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
-                                                     float* __restrict__ part_b, int rows, int E, DropSite drop) {
+                                                     float* __restrict__ part_b, int rows, int E, DropSite drop,
+                                                     int drop_res) {
     __shared__ float red[2][LN_WAVES_BWD][NV * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 pg[NV], pb[NV], gm[NV];
@@ -163,11 +164,18 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                 v.y += r * (g[i].y - c2 - h.y * c1);
                 v.z += r * (g[i].z - c2 - h.z * c1);
                 v.w += r * (g[i].w - c2 - h.w * c1);
+                if (drop_res && drop.thresh) {  // final residual gradient taken through the branch dropout
+                    const unsigned k = drop_keep4(drop, row, c);
+                    v.x = (k & 1u) ? v.x * drop.scale : 0.f;
+                    v.y = (k & 2u) ? v.y * drop.scale : 0.f;
+                    v.z = (k & 4u) ? v.z * drop.scale : 0.f;
+                    v.w = (k & 8u) ? v.w * drop.scale : 0.f;
+                }
                 *reinterpret_cast<float4*>(dres + (size_t)row * E + c) = v;
                 if (dres_b) {
                     bf16x4 ob;
                     float4 u = v;
-                    if (drop.thresh) {
+                    if (drop.thresh && !drop_res) {
                         const unsigned k = drop_keep4(drop, row, c);
                         u.x = (k & 1u) ? u.x * drop.scale : 0.f;
                         u.y = (k & 2u) ? u.y * drop.scale : 0.f;
@@ -386,21 +394,22 @@ extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {
 namespace ergm {
 // Main LayerNorm-backward pass only: dres += dx, dres_bf16, and per-block dγ/dβ partials
 // (part_g/part_b: ln_bwd_nparts(rows) x E floats each), reduced later by layernorm_param_reduce.
+// drop_res: the updated dres is final and itself goes through `drop` (dres_bf16 then gets the same values).
 int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
 
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop) {
+                       const DropSite& drop, int drop_res) {
     if (diag_skip() & 32) return ERGM_OK;
     ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
-        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
-        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
-        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop); break;
+        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
     }
     return check_launch("layernorm_bwd");
 }
@@ -434,7 +443,7 @@ extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* 
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
     hipStream_t s = as_stream(stream);
-    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E)));
+    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E), 0));
     return layernorm_param_reduce(pg, pb, rows, E, dgamma, dbeta, s);
 }
 

@@ -150,26 +150,29 @@ struct GldsTile {
     static_assert(PER_WAVE >= 1 && PER_WAVE * 1024 * NWAVES == BYTES, "tile / wave count mismatch");
 
     // r0: tile origin along M|N; Rlim: M|N (valid extent); k0: K origin of the stage.
+    // Piece i (0 <= i < PER_WAVE) of this wave's share of the stage: one 1-KiB wave-instruction.
+    __device__ __forceinline__ static void issue_piece(char* lds, const __bf16* base, int ld, int r0, int Rlim, int k0,
+                                                       int wave, int i) {
+        const int lane = threadIdx.x & 63;
+        const int ib = (i * NWAVES + wave) * 1024;
+        const int o = ib + lane * 16;
+        const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
+        const __bf16* src;
+        if (!TRANS) {
+            const int c = pc ^ swz_row(row);
+            const int r = min(r0 + row, Rlim - 1);
+            src = base + (size_t)r * ld + k0 + c * 8;
+        } else {
+            const int c = pc ^ (CPR == 16 ? swz_tr16(row) : swz_tr8(row));
+            const int col = min(r0 + c * 8, ((Rlim + 7) & ~7) - 8);
+            src = base + (size_t)(k0 + row) * ld + col;
+        }
+        glds16(src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + ib)));
+    }
     __device__ __forceinline__ static void issue(char* lds, const __bf16* base, int ld, int r0, int Rlim, int k0,
                                                  int wave) {
-        const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int i = 0; i < PER_WAVE; ++i) {
-            const int ib = (i * NWAVES + wave) * 1024;
-            const int o = ib + lane * 16;
-            const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
-            const __bf16* src;
-            if (!TRANS) {
-                const int c = pc ^ swz_row(row);
-                const int r = min(r0 + row, Rlim - 1);
-                src = base + (size_t)r * ld + k0 + c * 8;
-            } else {
-                const int c = pc ^ (CPR == 16 ? swz_tr16(row) : swz_tr8(row));
-                const int col = min(r0 + c * 8, ((Rlim + 7) & ~7) - 8);
-                src = base + (size_t)(k0 + row) * ld + col;
-            }
-            glds16(src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + ib)));
-        }
+        for (int i = 0; i < PER_WAVE; ++i) issue_piece(lds, base, ld, r0, Rlim, k0, wave, i);
     }
 };
 

@@ -333,6 +333,28 @@ extern "C" int ergm_loss_finalize(const float* row_loss, int T, const int* n_val
 }
 
 namespace ergm {
+// dl[i] = bf16(scale · dl[i] + g[i]) over n bf16 elements (8 per thread): a caller's gradient on the returned
+// logits added to the cross-entropy's, both scaled as the LM-head backward GEMMs expect (alpha 1).
+__global__ __launch_bounds__(256) void dlogits_add_kernel(bf16x8* __restrict__ dl, const bf16x8* __restrict__ g,
+                                                          const float* __restrict__ scale, size_t n8) {
+    const float sc = scale ? *scale : 1.0f;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+        bf16x8 a = dl[i];
+        const bf16x8 b = g[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = f2bf(sc * bf2f(a[j]) + bf2f(b[j]));
+        dl[i] = a;
+    }
+}
+int dlogits_add(void* dl, const void* g, const float* scale, size_t n, hipStream_t s) {
+    ERGM_CHECK_ARG(dl && g && n % 8 == 0 && aligned16(dl) && aligned16(g), "dlogits_add: bad argument");
+    const size_t n8 = n / 8;
+    const unsigned grid = (unsigned)std::min<size_t>((n8 + 255) / 256, 4096);
+    hipLaunchKernelGGL(dlogits_add_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<bf16x8*>(dl),
+                       reinterpret_cast<const bf16x8*>(g), scale, n8);
+    return check_launch("dlogits_add");
+}
+
 // ergm_loss_finalize that also accumulates the trainer metrics (ergm_model_set_metrics).
 int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
                           const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,

@@ -58,6 +58,7 @@ class DPSync:
         self._stream = None
         self._events: List = []
         self.grad_comm = grad_comm or os.environ.get("ERGM_DP_GRAD", "fp32")
+        self.force = process_group is not None and os.environ.get("ERGM_DP_FORCE", "0") == "1"
         if self.grad_comm not in ("bf16", "fp32"):
             raise ValueError(f"grad_comm must be 'bf16' or 'fp32' (got {self.grad_comm!r})")
         self._pool = None          # bf16 exchange buffers, reused in stream order by every reduction
@@ -77,6 +78,7 @@ class DPSync:
         self._master = None        # fp32 master whose directly-read elements stay replicated (set_master)
         self._mranges: List[Tuple[int, int]] = []
         self._midx: dict = {}
+        self._pend_master: List[Tuple[int, int, int, int]] = []
 
     def set_master(self, master: torch.Tensor, ranges: List[Tuple[int, int]]) -> None:
         """The fp32 master and the ranges of it the executor reads directly (params.master_read_ranges):
@@ -84,19 +86,35 @@ class DPSync:
         LayerNorm parameters, biases, wpe and emotion head on every rank (the shadow covers the rest)."""
         self._master, self._mranges, self._midx = master, list(ranges), {}
 
-    def _sync_master(self, a: int, b: int, lo: int, hi: int) -> None:
+    def _sync_master(self) -> None:
+        """Replicate the directly-read fp32 master elements of every range updated shard-wise this step: one
+        gather of the owners' values (non-owners contribute 0, so the SUM is the owner's value), ONE
+        all-reduce, one scatter — per step, on the comm stream after the last bucket's update (the next
+        forward is the first reader).  Round 2 did this per exchanged bucket (index build, where, all-reduce,
+        index_put each time: ~0.1 ms of host work per bucket)."""
         import torch.distributed as dist
-        key = (a, b)
-        if key not in self._midx:
-            parts = [torch.arange(max(a, s), min(b, e)) for s, e in self._mranges if s < b and e > a]
-            idx = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.long)
-            own = (idx >= a + lo) & (idx < a + hi)
-            self._midx[key] = (idx.to(self._master.device), own.to(self._master.device))
-        idx, own = self._midx[key]
-        if idx.numel() == 0:
+        pend, self._pend_master = self._pend_master, []
+        if not pend or self._master is None:
             return
-        # each element has exactly one owner; the others contribute 0, so the SUM is the owner's value
-        vals = torch.where(own, self._master[idx], torch.zeros((), dtype=self._master.dtype, device=idx.device))
+        key = tuple(pend)
+        if key not in self._midx:
+            idx, own = [], []
+            for a, b, lo, hi in pend:
+                for s, e in self._mranges:
+                    if s < b and e > a:
+                        r = torch.arange(max(a, s), min(b, e))
+                        idx.append(r)
+                        own.append((r >= a + lo) & (r < a + hi))
+            if not idx:
+                self._midx[key] = None
+            else:
+                i, o = torch.cat(idx), torch.cat(own)
+                self._midx[key] = (i.to(self._master.device), o.to(self._master.device, self._master.dtype))
+        ent = self._midx[key]
+        if ent is None:
+            return
+        idx, own = ent
+        vals = self._master[idx] * own
         self.bytes_per_step += 2 * (self.world - 1) * vals.numel() * 4 // self.world
         if vals.is_cuda:
             dist.all_reduce(vals, group=self.pg, async_op=True).wait()
@@ -120,7 +138,11 @@ class DPSync:
 
     @property
     def active(self) -> bool:
-        return self.world > 1
+        """Data-parallel schedule on: more than one rank, or ERGM_DP_FORCE=1 with a process group of one
+        (the whole exchange schedule — collectives on the comm stream, compact lookup block, per-bucket
+        updates — runs against a world-1 communicator: on the one-GPU box this exercises ProcessGroupNCCL,
+        i.e. RCCL, which refuses two ranks on one device)."""
+        return self.world > 1 or self.force
 
     def reduce_count(self, counts: torch.Tensor) -> None:
         """In place: local valid-label counts (LM, emotion) -> global counts (before the forward).
@@ -132,6 +154,7 @@ class DPSync:
 
     def begin(self) -> None:
         self._works = []
+        self._pend_master = []
         self.bytes_per_step = 0
         self._pend_a = None
 
@@ -246,7 +269,7 @@ class DPSync:
                 post(a + lo, a + hi)
             self.gather_(shadow[a:b], lo, hi)
             if self._master is not None:
-                self._sync_master(a, b, lo, hi)
+                self._pend_master.append((a, b, lo, hi))  # replicated once per step (_sync_master)
             self.sharded.add((a, b))
             self.master_sharded.add((a, b))
             return
@@ -314,7 +337,15 @@ class DPSync:
         self.enqueue(grad, lambda: self.reduce_then(grad, a, b, post, shadow), k, wait)
 
     def finish(self, grad: torch.Tensor) -> None:
-        """Make the current stream wait for every outstanding bucket (no host synchronisation)."""
+        """Replicate the sharded updates' directly-read master elements (one collective, on the comm stream
+        behind every bucket's update), then make the current stream wait for every outstanding bucket (no
+        host synchronisation)."""
+        if self._pend_master:
+            if grad.is_cuda:
+                with torch.cuda.stream(self._side(grad.device)):
+                    self._sync_master()
+            else:
+                self._sync_master()
         for w in self._works:
             w.wait()
         self._works = []

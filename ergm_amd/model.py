@@ -22,8 +22,9 @@ applied with counter-based masks (include/ergm_hip.h ergm_dropout); ``eval()`` d
 masks are drawn from ``torch``'s default generator at construction (``torch.manual_seed`` makes a run
 reproducible) and advance with every training forward.
 
-Differences from the reference, by design: ``logits`` come back as bf16 (the compute dtype) and are
-not differentiable (the reference trainer only back-propagates ``loss``); the KV-cache /
+``logits`` are fp32 and differentiable like the reference's (cast on first access from the bf16 GEMM
+output, ``logits_bf16``; a loss built on them back-propagates).  Differences from the reference, by
+design: ``emotion_logits`` are not differentiable (the trainer back-propagates ``loss``); the KV-cache /
 ``past_key_values``, ``attention_mask``, ``head_mask``, ``inputs_embeds`` and ``output_attentions``
 paths are not part of the training hot path and raise ``NotImplementedError``.  A second training
 forward of the same shape before the first one's backward raises in that backward (one set of saved
@@ -50,9 +51,14 @@ from .runtime import ModelRunner
 
 @dataclass
 class CausalLMOutputWithEmotionClassification:
-    """src/model.py:48-60 (fields the training path produces)."""
+    """src/model.py:48-60 (fields the training path produces).
+
+    ``logits`` is fp32 [B,S,V] and differentiable like the reference's (src/model.py:698,731): it is the
+    compute-dtype (bf16) GEMM output ``logits_bf16`` cast on first access, so a training step that never
+    reads it pays nothing; a loss built on it back-propagates through the fused backward (its gradient is
+    added to the cross-entropy's before the LM-head backward GEMMs)."""
     loss: Optional[torch.Tensor] = None
-    logits: Optional[torch.Tensor] = None
+    logits_bf16: Optional[torch.Tensor] = None    # [B,S,V] view of the bf16 GEMM output
     emotion_logits: Optional[torch.Tensor] = None
     past_key_values: Optional[tuple] = None
     hidden_states: Optional[tuple] = None
@@ -60,6 +66,13 @@ class CausalLMOutputWithEmotionClassification:
     cross_attentions: Optional[tuple] = None
     loss_lm: Optional[torch.Tensor] = None        # build extra: the LM part (PPL = exp(loss_lm))
     loss_emotion: Optional[torch.Tensor] = None   # build extra: the emotion CE part
+    _logits32: Optional[torch.Tensor] = None
+
+    @property
+    def logits(self) -> Optional[torch.Tensor]:
+        if self._logits32 is None and self.logits_bf16 is not None:
+            self._logits32 = self.logits_bf16.float()
+        return self._logits32
 
     def __getitem__(self, i):
         return (self.loss, self.logits, self.emotion_logits)[i]
@@ -114,15 +127,17 @@ def _(flat, ids, tt, cap_ids, vis, aud, labels, emo_labels, handle, key):
 
 
 @torch.library.custom_op("ergm::train_step_backward", mutates_args=())
-def _train_step_backward(flat: torch.Tensor, grad_loss: torch.Tensor, handle: int, key: List[int]) -> torch.Tensor:
-    """Gradient of the flat parameter buffer for the runner's last training forward (fresh tensor)."""
+def _train_step_backward(flat: torch.Tensor, grad_loss: torch.Tensor, grad_logits: Optional[torch.Tensor], handle: int,
+                         key: List[int]) -> torch.Tensor:
+    """Gradient of the flat parameter buffer for the runner's last training forward (fresh tensor);
+    ``grad_logits`` (bf16 [B*S, Vp] or None) is a gradient on the returned logits."""
     model = _model_of(handle)
-    model._runners[tuple(key)].backward(grad_loss)
+    model._runners[tuple(key)].backward(grad_loss, grad_logits=grad_logits)
     return model.grad_buf.clone()
 
 
 @_train_step_backward.register_fake
-def _(flat, grad_loss, handle, key):
+def _(flat, grad_loss, grad_logits, handle, key):
     return torch.empty_like(flat)
 
 
@@ -131,7 +146,7 @@ def _train_step_setup(ctx, inputs, output):
     ctx.handle, ctx.key = handle, key
     model = _MODELS.get(handle)
     ctx.fwd_id = model._runners[tuple(key)].fwd_count if model is not None and not _compiling(output[0]) else -1
-    ctx.mark_non_differentiable(output[1], output[2])
+    ctx.mark_non_differentiable(output[2])
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(inputs[0])
 
@@ -148,13 +163,19 @@ def _compiling(t: Optional[torch.Tensor] = None) -> bool:
 
 def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
     nones = (None,) * 9
-    if grad_loss is None:
+    if grad_loss is None and grad_logits is None:
         return (None,) + nones
-    gl = grad_loss.reshape(-1)[2:3] if grad_loss.numel() == 3 else grad_loss.reshape(1)
-    gl = gl.float().contiguous()
-    if _compiling(grad_loss):  # traced by AOTAutograd: the opaque backward op, its output accumulated by autograd
+    if grad_loss is None:  # only the logits were differentiated: the loss part contributes nothing
+        gl = torch.zeros(1, dtype=torch.float32, device=grad_logits.device)
+    else:
+        gl = grad_loss.reshape(-1)[2:3] if grad_loss.numel() == 3 else grad_loss.reshape(1)
+        gl = gl.float().contiguous()
+    if grad_logits is not None:
+        grad_logits = grad_logits.to(torch.bfloat16).contiguous()
+    if _compiling(gl):  # traced by AOTAutograd: the opaque backward op, its output accumulated by autograd
+        # (AOTAutograd hands every differentiable output a tangent, zeros when the loss ignores the logits)
         flat, = ctx.saved_tensors
-        return (torch.ops.ergm.train_step_backward(flat, gl, ctx.handle, ctx.key),) + nones
+        return (torch.ops.ergm.train_step_backward(flat, gl, grad_logits, ctx.handle, ctx.key),) + nones
     model = _model_of(ctx.handle)
     runner = model._runners[tuple(ctx.key)]
     if runner.fwd_count != ctx.fwd_id:
@@ -172,7 +193,7 @@ def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
                 post = opt._backward_hook(flat, model)   # after each bucket's exchange (Python, comm stream)
             else:
                 native = opt._native_desc(flat, model)   # scheduled by the executor
-        runner.backward(gl, post, native)            # writes model.grad_buf
+        runner.backward(gl, post, native, grad_logits)  # writes model.grad_buf
         if native is not None and native.defer:
             model._deferred = runner                 # its block updates are still running (next forward waits)
         flat.grad = model.grad_buf
@@ -180,10 +201,10 @@ def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
         # accumulate semantics when the caller did not zero the gradient
         tmp = model._grad_tmp()
         tmp.copy_(model.grad_buf)                    # the gradient accumulated so far
-        runner.backward(gl)                          # overwrites grad_buf with this backward's
+        runner.backward(gl, grad_logits=grad_logits)  # overwrites grad_buf with this backward's
         ops.axpy(tmp, model.grad_buf)
     else:
-        runner.backward(gl)
+        runner.backward(gl, grad_logits=grad_logits)
         ops.axpy(model.grad_buf, flat.grad)
     return (None,) + nones
 
@@ -465,7 +486,7 @@ class GPT2LMHeadModel(nn.Module):
         else:
             logits, emo, loss3 = runner.forward(ids, tt, cap, vis, aud, lab, emo_lab, train=False)
         out = CausalLMOutputWithEmotionClassification(
-            logits=logits.view(B, S, Vp)[:, :, :V], emotion_logits=emo)
+            logits_bf16=logits.view(B, S, Vp)[:, :, :V], emotion_logits=emo)
         if loss3 is not None:
             out.loss = loss3[2] if lab is not None or emo_lab is not None else None
             out.loss_lm = loss3[0].detach() if lab is not None else None

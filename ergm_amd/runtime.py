@@ -194,7 +194,8 @@ class ModelRunner:
         return logits, emo, loss
 
     # ---- backward -----------------------------------------------------------------------
-    def backward(self, grad_scale: Optional[torch.Tensor], post=None, native_opt=None) -> None:
+    def backward(self, grad_scale: Optional[torch.Tensor], post=None, native_opt=None,
+                 grad_logits: Optional[torch.Tensor] = None) -> None:
         """Writes every parameter gradient into self.grad (overwrite, not accumulate).  With a
         process group, each bucket is all-reduced (SUM) on a side stream as soon as it is final.
 
@@ -209,6 +210,8 @@ class ModelRunner:
         # single process: the executor runs the per-bucket AdamW schedule itself (ergm_model_set_optimizer)
         L.check(lib.ergm_model_set_optimizer(self.plan, C.byref(native_opt) if native_opt is not None else None),
                 "ergm_model_set_optimizer")
+        if grad_logits is not None:  # a loss built on the returned logits (bf16 [B*S, Vp], kept alive until here)
+            L.check(lib.ergm_model_set_logits_grad(self.plan, _p(grad_logits)), "ergm_model_set_logits_grad")
         L.check(lib.ergm_model_backward_head(self.plan, _p(grad_scale), s), "ergm_model_backward_head")
         Lyr, E, Vp = self.layout.L, self.layout.E, self.layout.vocab_pad
         compact = self.compact_lookup

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 4
+#define ERGM_ABI_VERSION 5
 
 typedef enum {
     ERGM_OK = 0,
@@ -255,18 +255,20 @@ int ergm_loss_finalize(const float* row_loss, int T, const int* n_valid_global,
 /* torch.optim.AdamW step over flat fp32 arrays; also refreshes the bf16 shadow copy.
  * Arithmetic in torch's order: p*=(1-lr·wd); m=lerp(m,g,1-β1); v=β2·v+(1-β2)g²;
  * p -= step_size · m / (sqrt(v)/bc2_sqrt + eps), step_size = lr/(1-β1^t), bc2_sqrt = sqrt(1-β2^t).
+ * lr, β1, β2 and weight_decay are doubles (ABI 5): torch forms 1-lr·wd, 1-β1 and 1-β2 from the Python
+ * doubles and rounds each once to fp32 (from a float β2 = 0.999f, 1-β2 is off by 1.3e-5 relative).
  * max_blocks > 0 caps the grid (grid-stride loop): an update running concurrently with the backward
  * on another stream then occupies only that many CUs instead of flooding the chip; 0 = full grid. */
-int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, float lr,
-                    float beta1, float beta2, float eps, float weight_decay, float step_size,
+int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, double lr,
+                    double beta1, double beta2, float eps, double weight_decay, float step_size,
                     float bc2_sqrt, int max_blocks, void* stream);
 /* The same update restricted to the rows of a [rows][row_len] block whose flag byte matches:
  * row r is updated iff (row_flag[r] != 0) == (select != 0).  With ergm_model_set_row_flags this
  * splits the tied-embedding update into the rows only the LM head touched (final early in the
  * backward) and the rows the lookups touched (final after the embedding backward). */
 int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
-                    const void* row_flag, int select, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream);
+                    const void* row_flag, int select, double lr, double beta1, double beta2, float eps,
+                    double weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream);
 /* bf16 shadow copy of fp32 values: dst[i] = bf16(src[i]). */
 int ergm_cast_bf16(const float* src, void* dst, size_t n, void* stream);
 /* y[i] += x[i] (f32), used to accumulate gradients across backward calls. */
@@ -406,7 +408,8 @@ typedef struct {
     const int64_t* ranges;    /* [n_ranges][2] element ranges [a, b) */
     int n_ranges;             /* n_layer + 1 */
     int64_t wte_begin;        /* element offset of the tied wte */
-    float lr, beta1, beta2, eps, weight_decay;
+    double lr, beta1, beta2, weight_decay;  /* doubles as torch holds them (ABI 5) */
+    float eps;
     float step_size;          /* lr / (1 - beta1^t) */
     float bc2_sqrt;           /* sqrt(1 - beta2^t) */
     int max_blocks;           /* grid cap of each update, 0 = none */
@@ -432,6 +435,11 @@ int ergm_model_set_side_joins(ergm_model_plan* plan, int per_stage);
  * loss_acc[1] and its number of samples with argmax(emotion_logits) == emotion_labels (first maximum, as
  * torch.argmax) to *correct, in the loss finalisation (no extra launch).  nullptr pointers: off.      */
 int ergm_model_set_metrics(ergm_model_plan* plan, float* loss_acc, int64_t* correct);
+/* A caller's gradient on the logits of the last training forward (bf16 [B*S][vocab_pad], pad columns 0;
+ * src/model.py:698 returns differentiable logits): the next ergm_model_backward_head adds it to the
+ * cross-entropy's dlogits (dlogits = bf16(grad_scale · dlogits + grad_logits)) before the LM-head backward
+ * GEMMs, then forgets it.  NULL: none (default).  The buffer must stay valid until that call. */
+int ergm_model_set_logits_grad(ergm_model_plan* plan, const void* grad_logits);
 int ergm_model_stage_wait(ergm_model_plan* plan, int stage, void* stream);
 
 /* Kernel probe for in-loop timing: while set, the executor records `ev_begin` / `ev_end`

@@ -189,3 +189,57 @@ def test_dp2_dropout_and_trainer_metrics_match_single_process(gpu):
     assert abs(r["loss"] - r["ref_loss"]) <= 1e-3 * abs(r["ref_loss"]), (r["loss"], r["ref_loss"])
     assert abs(r["ppl"] - r["ref_ppl"]) <= 1e-2 * r["ref_ppl"], (r["ppl"], r["ref_ppl"])
     assert abs(r["acc"] - r["ref_acc"]) <= 100.0 / (2 * B) + 1e-9, (r["acc"], r["ref_acc"])
+
+
+def _worker_nccl_world1(rank, world, port, out_path, mode):
+    """ProcessGroupNCCL (RCCL) on the real box: a world-1 "nccl" group with the data-parallel schedule forced
+    on (ERGM_DP_FORCE=1): counts all-reduced, gradient buckets exchanged on the comm stream (all_reduce, or
+    all_to_all_single + all_gather_into_tensor for bf16), the compact wte lookup block, per-bucket updates
+    after each exchange — against the same model without a process group, in the same process."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ERGM_DP_FORCE="1",
+                      ERGM_DP_GRAD="fp32" if mode == "fp32" else "bf16", ERGM_DP_ZERO="1" if mode == "bf16z" else "0")
+    import torch.distributed as dist
+    from ergm_amd.model import GPT2LMHeadModel
+    from ergm_amd.optim import FusedAdamW
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    res = {}
+    for tag, pg in (("dp", dist.group.WORLD), ("ref", None)):
+        model = GPT2LMHeadModel(_cfg(), device=dev, process_group=pg)
+        model.init_weights(seed=3)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
+        grads = [_step(model, opt, b, dev).cpu() for b in (_batch(), {k: v.roll(1, 0) for k, v in _batch().items()})]
+        active = next(iter(model._runners.values())).dp.active
+        model.consolidate_()
+        torch.cuda.synchronize()
+        st = opt.state[model.flat]
+        res[tag] = dict(grads=grads, flat=model.flat.detach().cpu(), m=st["exp_avg"].cpu(), v=st["exp_avg_sq"].cpu(),
+                        shadow=model.flat_b16.cpu(), active=active)
+    dist.destroy_process_group()
+    torch.save(res, out_path)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16z"])
+def test_nccl_world1_forced_dp_matches_single_process(gpu, mode):
+    """fp32: bitwise the single-process step (a world-1 all-reduce is the identity and the per-bucket
+    updates are the executor's arithmetic); bf16 / bf16 + ZeRO-1: the gradient rounded to bf16 once, so
+    within the bf16 exchange gate."""
+    torch.cuda.synchronize()
+    path = os.path.join(tempfile.mkdtemp(), "n1.pt")
+    mp.spawn(_worker_nccl_world1, args=(1, _free_port(), path, mode), nprocs=1, join=True)
+    r = torch.load(path, weights_only=True)
+    dp, ref = r["dp"], r["ref"]
+    assert dp["active"] and not ref["active"]
+    if mode == "fp32":
+        for k in ("flat", "m", "v", "shadow"):
+            assert torch.equal(dp[k], ref[k]), k
+        for a, b in zip(dp["grads"], ref["grads"]):
+            assert torch.equal(a, b)
+    else:
+        for a, b in zip(dp["grads"], ref["grads"]):
+            err = ((a - b).norm() / b.norm()).item()
+            assert err < 4e-3, err
+        p0 = torch.zeros(0)
+        d = ((dp["flat"] - ref["flat"]).norm() / ref["flat"].norm()).item()
+        assert d < 1e-3, d

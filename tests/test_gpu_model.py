@@ -547,3 +547,32 @@ def test_custom_op_registration_and_torch_compile(gpu):
         outs.append((out.loss.detach().clone(), out.logits.clone(), model.flat.grad.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_logits_are_fp32_and_differentiable(gpu):
+    """src/model.py:698,731 returns fp32 logits with autograd: outputs.logits is fp32 and a loss built on it
+    back-propagates through the fused backward (the caller's logits gradient is added to the cross-entropy's
+    before the LM-head GEMMs).  Against the oracle's gradient of the same combined loss; then the logits
+    alone (grad of loss is None)."""
+    rec = _load("tiny_e64.npz")
+    ocfg, cfg, P0, model, batch = _setup(rec, gpu)
+    kw = {k: v.to(gpu) for k, v in batch.items()}
+    R = torch.randn(batch["input_ids"].shape + (ocfg.vocab_size,), generator=torch.Generator().manual_seed(3))
+
+    def run(with_loss):
+        model.flat.grad = None
+        out = model(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                    emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw.get("visual_feat"),
+                    auds=kw.get("audio_feat"))
+        assert out.logits.dtype == torch.float32 and out.logits.requires_grad
+        extra = (out.logits * R.to(gpu)).sum() * 0.05
+        (out.loss + extra if with_loss else extra).backward()
+        torch.cuda.synchronize()
+        leaves = {k: v.clone().requires_grad_(True) for k, v in P0.items()}
+        o = O.forward(leaves, ocfg, **batch)
+        ext = (o["logits"] * R).sum() * 0.05
+        (o["loss"] + ext if with_loss else ext).backward()
+        # parameters the logits do not depend on (the emotion head) get no oracle gradient: zero
+        _grad_gate(_grads(model), {k: v.grad if v.grad is not None else torch.zeros_like(v) for k, v in leaves.items()})
+    run(True)
+    run(False)

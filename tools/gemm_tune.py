@@ -48,7 +48,9 @@ SHAPES = [
 CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (256, 256), (128, 64), (64, 128),
         (256, 128), (128, 128), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
         (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
-        (256, 256), (128, 128), (128, 128)]                       # 22-24 LDS-free epilogue variants
+        (256, 256), (128, 128), (128, 128),                       # 22-24 LDS-free epilogue variants
+        (64, 64), (128, 128), (128, 128), (256, 256), (64, 128), (128, 128), (128, 128), (128, 128),  # 25-32 IL
+        (64, 64), (64, 64), (64, 128), (128, 64), (128, 128)]                                         # 33-37 KS2
 REPS = 20
 
 
