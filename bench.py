@@ -331,6 +331,11 @@ def main():
     barrier()
     torch.cuda.synchronize()
     sync0 = sum(r.host_sync_s for r in model._runners.values())
+    prof = None
+    if os.environ.get("ERGM_BENCH_CPROFILE"):  # host-cost diagnostics: cProfile of the timed loop only
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if args.probe != 5:
@@ -338,6 +343,9 @@ def main():
             _lib.check(lib.ergm_model_set_probe(runner.plan, args.probe, e0.ev, e1.ev), "ergm_model_set_probe")
         step()
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (≈ dt when host-bound)
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["ERGM_BENCH_CPROFILE"])
     t_sync = sum(r.host_sync_s for r in model._runners.values()) - sync0  # of it: waiting (DP row count)
     torch.cuda.synchronize()
     barrier()

@@ -104,6 +104,7 @@ _SIGS = {
     "ergm_cast_bf16": (i32, [vp, vp, sz, vp]),
     "ergm_axpy": (i32, [vp, vp, sz, f32, vp]),
     "ergm_chunk_sum_bf16": (i32, [vp, i32, sz, vp, vp]),
+    "ergm_chunk_sum_bf16_f32": (i32, [vp, i32, sz, sz, vp, vp]),
     "ergm_cast_f32": (i32, [vp, vp, sz, vp]),
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),

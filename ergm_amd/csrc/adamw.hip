@@ -237,6 +237,20 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(const bf16x4* __restrict
     }
 }
 
+// The same sum, rounded once to bf16 and written back widened to fp32 straight into the gradient (ZeRO-1:
+// this rank's reduced chunk), for the first n4 groups only (the last rank's chunk may be short).
+__global__ __launch_bounds__(256) void chunk_sum_f32_kernel(const bf16x4* __restrict__ in, int nchunks, size_t chunk4,
+                                                            size_t n4, float4* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < nchunks; ++j) {
+            const bf16x4 v = in[(size_t)j * chunk4 + i];
+            s.x += bf2f(v[0]); s.y += bf2f(v[1]); s.z += bf2f(v[2]); s.w += bf2f(v[3]);
+        }
+        out[i] = make_float4(bf2f(f2bf(s.x)), bf2f(f2bf(s.y)), bf2f(f2bf(s.z)), bf2f(f2bf(s.w)));
+    }
+}
+
 __global__ __launch_bounds__(256) void cast_f32_kernel(const bf16x4* __restrict__ src, float4* __restrict__ dst,
                                                        size_t n4) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
@@ -253,6 +267,16 @@ extern "C" int ergm_chunk_sum_bf16(const void* in, int nchunks, size_t chunk, vo
     hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(c4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
                        nchunks, c4, (bf16x4*)out);
     return check_launch("chunk_sum_bf16");
+}
+
+extern "C" int ergm_chunk_sum_bf16_f32(const void* in, int nchunks, size_t chunk, size_t n, float* out, void* stream) {
+    ERGM_CHECK_ARG(in && out && nchunks > 0 && chunk % 4 == 0 && n % 4 == 0 && n <= chunk,
+                   "chunk_sum_bf16_f32: bad argument");
+    const size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    hipLaunchKernelGGL(chunk_sum_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
+                       nchunks, chunk / 4, n4, (float4*)out);
+    return check_launch("chunk_sum_bf16_f32");
 }
 
 extern "C" int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream) {

@@ -131,7 +131,11 @@ struct ergm_model_plan {
     int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
     bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
     bool dw_group;  // ... and a qualifying pair as ONE grouped launch (gemm_dw_pair)
-    int capkv_split = 1;  // ERGM_CAPKV_SPLIT: caption K/V gradients per block stage (1) or stacked at the end (0)
+    // ERGM_CAPKV_SPLIT=1: the caption K/V gradients per block stage instead of stacked at the end — measured
+    // 0.25 ms/step SLOWER at C2 (6.04-6.14 vs 5.80-5.83 ms, 3 interleaved rounds, profiles/r03_experiments.txt):
+    // the backward is throughput-bound on the data- and weight-gradient streams, and 12 small GEMMs on each
+    // cost more there than the two large ones at the end, where they overlap the optimizer tail
+    int capkv_split = 0;
     int opt_lag = 2;  // ERGM_OPT_LAG: stages between a block's backward and its AdamW launch (opt_after_layer)
     std::vector<DwJob> dw_pend;
     bool bwd_forked;

@@ -237,8 +237,23 @@ class DPSync:
     def reduce_scatter_(self, t: torch.Tensor) -> Tuple[int, int]:
         """bf16 exchange without the all-gather: t[lo:hi] (this rank's chunk, returned) = Σ over ranks;
         the rest of t keeps the local gradient."""
-        mine, chunk, gath = self._exchange(t)
         lo, hi = self.shard(t.numel())
+        if t.is_cuda:  # cast + all-to-all, then ONE kernel: rank-order sum, bf16 rounding, widened into t[lo:hi]
+            import torch.distributed as dist
+            from . import _lib as L
+            W, n = self.world, t.numel()
+            chunk = self.chunk(n)
+            send, recv, _ = self._buffers(chunk, t.device)
+            self.bytes_per_step += (W - 1) * chunk * 2
+            st = C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+            if W * chunk > n:
+                send[n:].zero_()
+            L.call("ergm_cast_bf16", C.c_void_p(t.data_ptr()), C.c_void_p(send.data_ptr()), n, st)
+            dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+            L.call("ergm_chunk_sum_bf16_f32", C.c_void_p(recv.data_ptr()), W, chunk, hi - lo,
+                   C.c_void_p(t.data_ptr() + 4 * lo), st)
+            return lo, hi
+        mine, chunk, gath = self._exchange(t)
         self._cast_f32(mine, t[lo:hi])
         return lo, hi
 
@@ -265,9 +280,19 @@ class DPSync:
         when enabled, otherwise on the whole all-reduced range."""
         if self.active and self.zero and post is not None and shadow is not None:
             lo, hi = self.reduce_scatter_(grad[a:b])
-            if hi > lo:
-                post(a + lo, a + hi)
-            self.gather_(shadow[a:b], lo, hi)
+            if grad.is_cuda:  # the update writes its bf16 shadow chunk straight into its all-gather slot
+                n = b - a
+                chunk = self.chunk(n)
+                gath = self._buffers(chunk, grad.device)[2]
+                mine = gath.view(self.world, chunk)[self.rank]
+                if hi > lo:
+                    post(a + lo, a + hi, shadow_out=mine[:hi - lo])
+                self._gather(gath, mine)
+                shadow[a:b].copy_(gath[:n])
+            else:
+                if hi > lo:
+                    post(a + lo, a + hi)
+                self.gather_(shadow[a:b], lo, hi)
             if self._master is not None:
                 self._pend_master.append((a, b, lo, hi))  # replicated once per step (_sync_master)
             self.sharded.add((a, b))

@@ -145,9 +145,12 @@ class FusedAdamW(torch.optim.Optimizer):
         self._applied.add(id(flat))
         nb = self.overlap_blocks
 
-        def post(a, b, rows=None):
+        def post(a, b, rows=None, shadow_out=None):
+            # shadow_out: where the updated bf16 copy of flat[a:b] goes instead of the shadow (ZeRO-1: this
+            # rank's all-gather slot, from which the exchange writes every rank's chunk into the shadow)
             if rows is None:
-                ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], lr, b1, b2, eps, wd, t, nb)
+                ops.adamw_step(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b] if shadow_out is None else shadow_out,
+                               lr, b1, b2, eps, wd, t, nb)
             else:  # (row_len, row_flag, select): only the selected rows of the [.., row_len] block
                 row_len, flags, select = rows
                 ops.adamw_rows(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], row_len, flags, select, lr, b1,

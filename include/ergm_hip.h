@@ -277,6 +277,9 @@ int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* stream);
  * all-to-all of bf16 gradient chunks, out[i] = bf16(Σ_{j < nchunks} in[j·chunk + i]) summed in fp32
  * in rank order j; after the all-gather, dst[i] = f32(src[i]).  chunk, n multiples of 4.           */
 int ergm_chunk_sum_bf16(const void* in, int nchunks, size_t chunk, void* out, void* stream);
+/* ZeRO-1 reduce-scatter tail: the same rank-order fp32 sum of the nchunks copies, rounded once to bf16 and
+ * written widened to fp32 (out[i], i < n <= chunk, n % 4 == 0): this rank's reduced gradient chunk. */
+int ergm_chunk_sum_bf16_f32(const void* in, int nchunks, size_t chunk, size_t n, float* out, void* stream);
 int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

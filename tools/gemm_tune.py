@@ -20,16 +20,18 @@ if "--c5" in sys.argv:  # config 5 geometry (GPT-2-medium, B=32, S=128); its for
 if "--c4" in sys.argv:  # config 4 geometry (GPT-2-small, B=8, S=512)
     T = 4096
 L2E = 2 * E * LYR
+# --chain: the forward block GEMMs at the in-step row count (the forward runs as two batch-half chains)
+TF = T // 2 if "--chain" in sys.argv else T
 MK, KM, NK, KN = L.MK, L.KM, L.NK, L.KN
 BF, FP = L.BF16, L.F32
 # name, count/step, M, N, K, a_layout, lda, b_layout, ldb, epilogue, c_dtype
 SHAPES = [
     ("fwd capkv", 1, T, L2E, E, MK, E + 8, KN, L2E, L.EPI_BIAS, BF),
-    ("fwd c_attn", 12, T, 3 * E, E, MK, E + 8, KN, 3 * E, L.EPI_BIAS, BF),
-    ("fwd proj+resid", 24, T, E, E, MK, E + 8, KN, E, L.EPI_BIAS_RESID, FP),
-    ("fwd q_attn", 12, T, E, E, MK, E + 8, KN, E, L.EPI_BIAS, BF),
-    ("fwd c_fc+gelu", 12, T, F, E, MK, E + 8, KN, F, L.EPI_BIAS_GELU, BF),
-    ("fwd mlp proj+resid", 12, T, E, F, MK, F + 8, KN, E, L.EPI_BIAS_RESID, FP),
+    ("fwd c_attn", 12, TF, 3 * E, E, MK, E + 8, KN, 3 * E, L.EPI_BIAS, BF),
+    ("fwd proj+resid", 24, TF, E, E, MK, E + 8, KN, E, L.EPI_BIAS_RESID, FP),
+    ("fwd q_attn", 12, TF, E, E, MK, E + 8, KN, E, L.EPI_BIAS, BF),
+    ("fwd c_fc+gelu", 12, TF, F, E, MK, E + 8, KN, F, L.EPI_BIAS_GELU, BF),
+    ("fwd mlp proj+resid", 12, TF, E, F, MK, F + 8, KN, E, L.EPI_BIAS_RESID, FP),
     ("fwd lm_head", 1, T, VP, E, MK, E, NK, E, L.EPI_NONE, BF),
     ("bwd lm dX", 1, T, E, VP, MK, VP, KN, E, L.EPI_NONE, FP),
     ("bwd lm dW", 1, VP, E, T, KM, VP, KN, E, L.EPI_NONE, FP),
@@ -100,6 +102,8 @@ def main():
         if only_bwd and name.startswith("fwd") and name != "fwd lm_head":
             continue
         if only_dw and al != KM:
+            continue
+        if "--fwd" in sys.argv and not (name.startswith("fwd") and name not in ("fwd lm_head", "fwd capkv")):
             continue
         a_rows = M if al == MK else K
         b_rows = N if bl == NK else K
