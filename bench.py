@@ -224,6 +224,15 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if os.environ.get("ERGM_MAIN_CUMASK"):  # experiment hook: the caller's stream restricted to a CU mask
+        import ctypes as C
+        from ergm_amd import _lib
+        m = os.environ["ERGM_MAIN_CUMASK"]
+        words = [int(m[max(0, e - 8):e], 16) for e in range(len(m), 0, -8)]
+        sp = C.c_void_p()
+        if _lib._hip().hipExtStreamCreateWithCUMask(C.byref(sp), len(words), (C.c_uint32 * len(words))(*words)) != 0:
+            raise SystemExit("hipExtStreamCreateWithCUMask failed")
+        torch.cuda.set_stream(torch.cuda.ExternalStream(sp.value, device=dev))
     pg = None
     backend = None
     # host-cost hook (one-GPU box): ERGM_BENCH_FAKE_PG=N runs ONE process as rank 0 of a torch "fake" process

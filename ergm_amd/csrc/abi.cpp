@@ -11,6 +11,9 @@
 namespace ergm {
 
 static thread_local char g_err[512] = {0};
+thread_local LaunchBind g_bind;  // fork point bound to the next launches (common.h ERGM_LAUNCH)
+thread_local hipStream_t g_watch_s = nullptr;
+thread_local bool g_watch_dirty = true;
 
 int diag_skip() {
     static const int v = getenv("ERGM_DIAG_SKIP") ? atoi(getenv("ERGM_DIAG_SKIP")) : 0;

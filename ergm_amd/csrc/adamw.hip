@@ -169,11 +169,11 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     // #15); ERGM_ADAMW_NT=0 disables (A/B)
     static const bool nt = !getenv("ERGM_ADAMW_NT") || atoi(getenv("ERGM_ADAMW_NT")) != 0;
     if (nt)
-        hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
+        ERGM_LAUNCH(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
                            (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
                            one_m_b2, eps, step_size, bc2_sqrt);
     else
-        hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
+        ERGM_LAUNCH(adamw_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
                            (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
                            one_m_b2, eps, step_size, bc2_sqrt);
     return check_launch("adamw");
@@ -194,7 +194,7 @@ extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, voi
     float one_m_b2 = (float)(1.0 - beta2);
     unsigned grid = (unsigned)std::min(rows, 8192);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
-    hipLaunchKernelGGL(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+    ERGM_LAUNCH(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, rows, row_len / 4, (const uint8_t*)row_flag, select,
                        decay, one_m_b1, (float)beta2, one_m_b2, eps, step_size, bc2_sqrt);
     return check_launch("adamw_rows");
@@ -204,7 +204,7 @@ extern "C" int ergm_cast_bf16(const float* src, void* dst, size_t n, void* strea
     ERGM_CHECK_ARG(src && dst && n % 4 == 0, "cast_bf16: bad argument");
     size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
-    hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)src,
+    ERGM_LAUNCH(cast_bf16_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)src,
                        (bf16x4*)dst, n4);
     return check_launch("cast_bf16");
 }
@@ -213,7 +213,7 @@ extern "C" int ergm_axpy(const float* x, float* y, size_t n, float alpha, void* 
     ERGM_CHECK_ARG(x && y && n % 4 == 0, "axpy: bad argument");
     size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
-    hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)x, (float4*)y,
+    ERGM_LAUNCH(axpy_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const float4*)x, (float4*)y,
                        n4, alpha);
     return check_launch("axpy");
 }
@@ -264,7 +264,7 @@ extern "C" int ergm_chunk_sum_bf16(const void* in, int nchunks, size_t chunk, vo
     ERGM_CHECK_ARG(in && out && nchunks > 0 && chunk % 4 == 0, "chunk_sum_bf16: bad argument");
     const size_t c4 = chunk / 4;
     if (c4 == 0) return ERGM_OK;
-    hipLaunchKernelGGL(chunk_sum_kernel, dim3(grid_for(c4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
+    ERGM_LAUNCH(chunk_sum_kernel, dim3(grid_for(c4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
                        nchunks, c4, (bf16x4*)out);
     return check_launch("chunk_sum_bf16");
 }
@@ -274,7 +274,7 @@ extern "C" int ergm_chunk_sum_bf16_f32(const void* in, int nchunks, size_t chunk
                    "chunk_sum_bf16_f32: bad argument");
     const size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
-    hipLaunchKernelGGL(chunk_sum_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
+    ERGM_LAUNCH(chunk_sum_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in,
                        nchunks, chunk / 4, n4, (float4*)out);
     return check_launch("chunk_sum_bf16_f32");
 }
@@ -283,7 +283,7 @@ extern "C" int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream
     ERGM_CHECK_ARG(src && dst && n % 4 == 0, "cast_f32: bad argument");
     const size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
-    hipLaunchKernelGGL(cast_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)src,
+    ERGM_LAUNCH(cast_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)src,
                        (float4*)dst, n4);
     return check_launch("cast_f32");
 }

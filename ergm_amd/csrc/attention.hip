@@ -841,7 +841,7 @@ int g_attn_ns = getenv("ERGM_ATTN_NS") ? atoi(getenv("ERGM_ATTN_NS")) : 0;
 
 template <bool CAUSAL, int NS, bool DROP>
 void launch_tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
-    hipLaunchKernelGGL((attn_fwd_kernel<CAUSAL, NS, DROP>), grid, dim3(256), 0, s, a);
+    ERGM_LAUNCH((attn_fwd_kernel<CAUSAL, NS, DROP>), grid, dim3(256), 0, s, a);
 }
 // Defaults: 2 stages everywhere (tools/attn_bench.py at the C4 shape: forward fastest at 2, the dK/dV
 // kernel then fits 3 waves per SIMD without spills; dQ 3 isolated, 2 inside the C4 step, #20).
@@ -854,12 +854,12 @@ void tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
 template <bool CAUSAL, bool DROP>
 void tiled_bwd(dim3 gk, dim3 gq, hipStream_t s, const AttnArgs& a) {
     const int ns_kv = g_attn_ns ? g_attn_ns : 2, ns_q = g_attn_ns ? g_attn_ns : 2;
-    if (ns_kv == 3) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 3, DROP>), gk, dim3(256), 0, s, a);
-    else if (ns_kv == 4) hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 4, DROP>), gk, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dkv_kernel<CAUSAL, 2, DROP>), gk, dim3(256), 0, s, a);
-    if (ns_q == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 2, DROP>), gq, dim3(256), 0, s, a);
-    else if (ns_q == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 4, DROP>), gq, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<CAUSAL, 3, DROP>), gq, dim3(256), 0, s, a);
+    if (ns_kv == 3) ERGM_LAUNCH((attn_bwd_dkv_kernel<CAUSAL, 3, DROP>), gk, dim3(256), 0, s, a);
+    else if (ns_kv == 4) ERGM_LAUNCH((attn_bwd_dkv_kernel<CAUSAL, 4, DROP>), gk, dim3(256), 0, s, a);
+    else ERGM_LAUNCH((attn_bwd_dkv_kernel<CAUSAL, 2, DROP>), gk, dim3(256), 0, s, a);
+    if (ns_q == 2) ERGM_LAUNCH((attn_bwd_dq_kernel<CAUSAL, 2, DROP>), gq, dim3(256), 0, s, a);
+    else if (ns_q == 4) ERGM_LAUNCH((attn_bwd_dq_kernel<CAUSAL, 4, DROP>), gq, dim3(256), 0, s, a);
+    else ERGM_LAUNCH((attn_bwd_dq_kernel<CAUSAL, 3, DROP>), gq, dim3(256), 0, s, a);
 }
 // Dropout fields of AttnArgs from the C-ABI descriptor (rows (b·H + h)·Sq + q, cols Sk).
 int set_drop(AttnArgs& a, const ergm_dropout* d, void* keep_bits) {
@@ -941,16 +941,16 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
         }
         dim3 grid(1, H, B);
         if (causal) {
-            if (drop) hipLaunchKernelGGL((attn_bwd_short_kernel<true, true>), grid, dim3(512), AS_LDS, s, a);
-            else hipLaunchKernelGGL((attn_bwd_short_kernel<true, false>), grid, dim3(512), AS_LDS, s, a);
+            if (drop) ERGM_LAUNCH((attn_bwd_short_kernel<true, true>), grid, dim3(512), AS_LDS, s, a);
+            else ERGM_LAUNCH((attn_bwd_short_kernel<true, false>), grid, dim3(512), AS_LDS, s, a);
         } else {
-            if (drop) hipLaunchKernelGGL((attn_bwd_short_kernel<false, true>), grid, dim3(512), AS_LDS, s, a);
-            else hipLaunchKernelGGL((attn_bwd_short_kernel<false, false>), grid, dim3(512), AS_LDS, s, a);
+            if (drop) ERGM_LAUNCH((attn_bwd_short_kernel<false, true>), grid, dim3(512), AS_LDS, s, a);
+            else ERGM_LAUNCH((attn_bwd_short_kernel<false, false>), grid, dim3(512), AS_LDS, s, a);
         }
         return check_launch("attn_bwd");
     }
     dim3 gk(cdiv(Sk, AT_T), H, B), gq(cdiv(Sq, AT_T), H, B);
-    hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(B * Sq * H * 4, 256)), dim3(256), 0, s, a);
+    ERGM_LAUNCH(attn_delta_kernel, dim3(cdiv(B * Sq * H * 4, 256)), dim3(256), 0, s, a);
     if (causal) drop ? tiled_bwd<true, true>(gk, gq, s, a) : tiled_bwd<true, false>(gk, gq, s, a);
     else drop ? tiled_bwd<false, true>(gk, gq, s, a) : tiled_bwd<false, false>(gk, gq, s, a);
     return check_launch("attn_bwd");

@@ -1,6 +1,7 @@
 // Internal helpers shared by the gfx950 kernels of libergm_hip.so.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -23,6 +24,45 @@ int check_launch(const char* what);
     do {                               \
         int _rc = (expr);              \
         if (_rc != ERGM_OK) return _rc; \
+    } while (0)
+
+// ---- kernel launches, and fork points bound to them ------------------------------------------
+// Every kernel of the library is launched through ERGM_LAUNCH.  A cross-stream fork point made with
+// hipEventRecord puts a marker packet of its own on the producing stream, which the stream's next kernel
+// waits behind (~5 us per fork in the training step's backward); the same event bound to the producing
+// kernel's own dispatch (hipExtLaunchKernel's stop event) costs the stream nothing.  bind_arm(s, ev)
+// binds `ev` to every following ERGM_LAUNCH on stream s (so it ends up on the last one) until
+// bind_take(s) returns it; bind_take returns nullptr when nothing was launched on s since the arm or
+// the binding was cleared (bind_clear) — the caller then records the event itself.
+struct LaunchBind {
+    hipStream_t s = nullptr;
+    hipEvent_t armed = nullptr;  // bound to each ERGM_LAUNCH on s while set
+    bool bound = false;          // the latest launch on s carries `armed`
+};
+extern thread_local LaunchBind g_bind;
+// a taken fork point stays reusable while nothing is launched on its stream: watch_stream(s) starts watching,
+// ERGM_LAUNCH on the watched stream sets g_watch_dirty
+extern thread_local hipStream_t g_watch_s;
+extern thread_local bool g_watch_dirty;
+inline void watch_stream(hipStream_t s) { g_watch_s = s; g_watch_dirty = false; }
+inline void bind_arm(hipStream_t s, hipEvent_t ev) { g_bind = LaunchBind{s, ev, false}; }
+inline hipEvent_t bind_take(hipStream_t s) {
+    hipEvent_t e = (g_bind.armed && g_bind.bound && g_bind.s == s) ? g_bind.armed : nullptr;
+    g_bind = LaunchBind{};
+    return e;
+}
+inline void bind_clear() { g_bind = LaunchBind{}; }
+
+#define ERGM_LAUNCH(K, G, B, SH, S, ...)                                                        \
+    do {                                                                                        \
+        hipStream_t s_ = (S);                                                                   \
+        if (s_ == ::ergm::g_watch_s) ::ergm::g_watch_dirty = true;                              \
+        if (::ergm::g_bind.armed && s_ == ::ergm::g_bind.s) {                                   \
+            hipExtLaunchKernelGGL(K, G, B, SH, s_, nullptr, ::ergm::g_bind.armed, 0, __VA_ARGS__); \
+            ::ergm::g_bind.bound = true;                                                        \
+        } else {                                                                                \
+            hipLaunchKernelGGL(K, G, B, SH, s_, __VA_ARGS__);                                   \
+        }                                                                                       \
     } while (0)
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }

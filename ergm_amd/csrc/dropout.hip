@@ -69,7 +69,7 @@ int dropout_apply_f32(const DropSite& d, float* x, int rows, int cols, int ld, h
     ERGM_CHECK_ARG(x && rows > 0 && cols > 0 && cols % 4 == 0 && ld % 4 == 0 && ld >= cols && aligned16(x),
                    "dropout_apply: bad argument");
     const int64_t n = (int64_t)rows * (cols / 4);
-    hipLaunchKernelGGL(dropout_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, x, rows, cols, ld);
+    ERGM_LAUNCH(dropout_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, x, rows, cols, ld);
     return check_launch("dropout_apply");
 }
 
@@ -93,7 +93,7 @@ extern "C" int ergm_dropout_mask(const ergm_dropout* d, int rows, int cols, uint
     const DropSite s = make_drop_site(d->seed, d->offset, d->site, d->p, d->row0, cols);
     const int wpr = (cols + 31) / 32;
     const int64_t n = (int64_t)rows * wpr;
-    hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), s, rows,
+    ERGM_LAUNCH(dropout_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), s, rows,
                        cols, wpr, bits);
     return check_launch("dropout_mask");
 }

@@ -318,10 +318,10 @@ int embed_fwd_ld(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids, 
     ERGM_CHECK_ARG(ld_cap >= E && ld_cap % 4 == 0, "embed_fwd: bad ld_cap");
     auto* cb = reinterpret_cast<__bf16*>(cap);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
-        case 2: hipLaunchKernelGGL(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
-        case 3: hipLaunchKernelGGL(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
-        default: hipLaunchKernelGGL(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        case 1: ERGM_LAUNCH(embed_fwd_kernel<1>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        case 2: ERGM_LAUNCH(embed_fwd_kernel<2>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        case 3: ERGM_LAUNCH(embed_fwd_kernel<3>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
+        default: ERGM_LAUNCH(embed_fwd_kernel<4>, grid, dim3(256), 0, s, ids, tt, cap_ids, wte, wpe, vis, ld_vis, aud, h0, cb, ld_cap, B, S, E, V, drop); break;
     }
     return check_launch("embed_fwd");
 }
@@ -368,14 +368,14 @@ int embed_bwd_sort(const int64_t* ids, const int64_t* tt, const int64_t* cap_ids
     const int chunk = std::min(npad, SORT_MAX), nch = npad / chunk;
     const size_t lds = (size_t)chunk * sizeof(uint64_t);
     // (keys holds embed_sort_capacity(T) slots: n for one chunk, npad for several)
-    hipLaunchKernelGGL(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, 0, keys,
+    ERGM_LAUNCH(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, 0, keys,
                        nch > 1 ? npad : n, nch > 1 ? nullptr : row_flag);
     for (int size = 2 * chunk; size <= npad; size <<= 1) {
         for (int stride = size >> 1; stride >= chunk; stride >>= 1)
-            hipLaunchKernelGGL(embed_sort_global_kernel, dim3(cdiv(npad / 2, 256)), dim3(256), 0, s, keys, npad, size,
+            ERGM_LAUNCH(embed_sort_global_kernel, dim3(cdiv(npad / 2, 256)), dim3(256), 0, s, keys, npad, size,
                                stride);
         const bool last = size == npad;
-        hipLaunchKernelGGL(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, size, keys,
+        ERGM_LAUNCH(embed_sort_kernel, dim3(nch), dim3(1024), lds, s, ids, tt, cap_ids, T, V, chunk, size, keys,
                            last ? n : npad, last ? row_flag : nullptr);
     }
     return check_launch("embed_bwd_sort");
@@ -388,8 +388,8 @@ int embed_bwd_sums(const uint64_t* keys, int B, int S, int E, const float* dh0, 
     const int T = B * S, n = 3 * T;
     dim3 g1(cdiv(n, SEG_CH)), g2(n);
 #define ERGM_SEG(NC)                                                                                         \
-    hipLaunchKernelGGL(embed_runsum_kernel<NC>, g1, dim3(256), 0, s, keys, n, T, dh0, dcap, part, E);         \
-    hipLaunchKernelGGL(embed_segsum_kernel<NC>, g2, dim3(256), 0, s, keys, n, part, dwte, row_pos, E);
+    ERGM_LAUNCH(embed_runsum_kernel<NC>, g1, dim3(256), 0, s, keys, n, T, dh0, dcap, part, E);         \
+    ERGM_LAUNCH(embed_segsum_kernel<NC>, g2, dim3(256), 0, s, keys, n, part, dwte, row_pos, E);
     switch (cdiv(E, 256)) {
         case 1: ERGM_SEG(1) break;
         case 2: ERGM_SEG(2) break;
@@ -419,7 +419,7 @@ extern "C" int ergm_embed_bwd(const int64_t* ids, const int64_t* tt, const int64
 
 extern "C" int ergm_rows_scan(const void* row_flag, int n, int* pos, int* count, void* stream) {
     ERGM_CHECK_ARG(row_flag && pos && count && n > 0 && n <= 1024 * 1024, "rows_scan: bad argument");
-    hipLaunchKernelGGL(rows_scan_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (const uint8_t*)row_flag, n, pos,
+    ERGM_LAUNCH(rows_scan_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (const uint8_t*)row_flag, n, pos,
                        count);
     return check_launch("rows_scan");
 }
@@ -429,7 +429,7 @@ extern "C" int ergm_rows_compact(const void* row_flag, const int* pos, int n, in
     ERGM_CHECK_ARG(row_flag && pos && compact && n > 0 && row_len > 0 && row_len % 4 == 0, "rows_compact: bad argument");
     ERGM_CHECK_ARG(mode == 0 || (mode == 1 && dst), "rows_compact: mode 0 (zero) or 1 (scatter-add into dst)");
     ERGM_CHECK_ARG(aligned16(compact) && (!dst || aligned16(dst)), "rows_compact: 16-byte alignment");
-    hipLaunchKernelGGL(rows_compact_kernel, dim3(std::min(n, 8192)), dim3(256), 0, as_stream(stream),
+    ERGM_LAUNCH(rows_compact_kernel, dim3(std::min(n, 8192)), dim3(256), 0, as_stream(stream),
                        (const uint8_t*)row_flag, pos, n, row_len / 4, (float4*)compact, (float4*)dst, mode);
     return check_launch("rows_compact");
 }
@@ -466,14 +466,14 @@ __global__ __launch_bounds__(256) void proj_grad_pack_kernel(const float* __rest
 int feat_pack(const float* vis, int ld_vis, const float* aud, void* out, int B, int Bp, int Fd, int ld,
               hipStream_t s) {
     ERGM_CHECK_ARG(vis && aud && out && B > 0 && Bp >= B && ld > Fd, "feat_pack: bad argument");
-    hipLaunchKernelGGL(feat_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, vis, ld_vis, aud,
+    ERGM_LAUNCH(feat_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, vis, ld_vis, aud,
                        reinterpret_cast<__bf16*>(out), B, Bp, Fd, ld);
     return check_launch("feat_pack");
 }
 
 int proj_grad_pack(const float* dh0, void* d, int B, int Bp, int S, int E, hipStream_t s) {
     ERGM_CHECK_ARG(dh0 && d && B > 0 && Bp >= B && S >= 2, "proj_grad_pack: bad argument");
-    hipLaunchKernelGGL(proj_grad_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, dh0, reinterpret_cast<__bf16*>(d), B, Bp,
+    ERGM_LAUNCH(proj_grad_pack_kernel, dim3(2 * Bp), dim3(256), 0, s, dh0, reinterpret_cast<__bf16*>(d), B, Bp,
                        S, E);
     return check_launch("proj_grad_pack");
 }
@@ -519,8 +519,8 @@ extern "C" int ergm_feat_pool(const void* x, int x_dtype, int B, int T, int D, l
     dim3 grid(cdiv(D, 64), B);
     hipStream_t s = as_stream(stream);
     if (x_dtype == ERGM_BF16)
-        hipLaunchKernelGGL(feat_pool_kernel<true>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
+        ERGM_LAUNCH(feat_pool_kernel<true>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
     else
-        hipLaunchKernelGGL(feat_pool_kernel<false>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
+        ERGM_LAUNCH(feat_pool_kernel<false>, grid, dim3(256), 0, s, x, T, D, ld_t, ld_b, lengths, out, ld_out);
     return check_launch("feat_pool");
 }

@@ -1057,7 +1057,7 @@ static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
     (void)attr;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
     if (a.xcd_split) grid = dim3(8 * a.tiles_m * a.tiles_n, 1, 1);  // split == 8, slice = XCD
-    hipLaunchKernelGGL(split > 1 ? k_split : k_full, grid, dim3(nthreads), lds, s, a);
+    ERGM_LAUNCH(split > 1 ? k_split : k_full, grid, dim3(nthreads), lds, s, a);
 }
 
 template <bool AKM, bool BKN, int EPI, bool OB>
@@ -1116,9 +1116,9 @@ static void launch_reg(const GemmArgs& a, int split, hipStream_t s) {
     (void)attr;
     dim3 grid(a.tiles_m * a.tiles_n, 1, split);
     if (split > 1)
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
+        ERGM_LAUNCH((gemm_kernel<BM, BN, AKM, BKN, ERGM_EPI_NONE, false>), grid, dim3(GEMM_THREADS), lds, s, a);
     else
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, AKM, BKN, EPI, OB>), grid, dim3(GEMM_THREADS), lds, s, a);
+        ERGM_LAUNCH((gemm_kernel<BM, BN, AKM, BKN, EPI, OB>), grid, dim3(GEMM_THREADS), lds, s, a);
 }
 
 template <bool AKM, bool BKN, int EPI, bool OB>
@@ -1156,7 +1156,7 @@ template <int EPI, bool OB>
 static void launch_reduce(const GemmArgs& a, int split, hipStream_t s) {
     size_t total = (size_t)a.M * a.N;
     int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL((splitk_reduce_kernel<EPI, OB>), dim3(blocks), dim3(256), 0, s, a, split);
+    ERGM_LAUNCH((splitk_reduce_kernel<EPI, OB>), dim3(blocks), dim3(256), 0, s, a, split);
 }
 
 }  // namespace ergm
@@ -1185,7 +1185,7 @@ static void launch_f8_cfg(const GemmArgs& a, hipStream_t s) {
     auto k = gemm_f8_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, EPI, OB>;
     static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
     (void)attr;
-    hipLaunchKernelGGL(k, dim3(a.tiles_m * a.tiles_n), dim3(64 * c.wgm * c.wgn), lds, s, a);
+    ERGM_LAUNCH(k, dim3(a.tiles_m * a.tiles_n), dim3(64 * c.wgm * c.wgn), lds, s, a);
 }
 
 template <int EPI, bool OB>
@@ -1426,7 +1426,7 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     }
 #undef ERGM_EPI_CASE
     if (d->bias_grad && !cs_in)
-        hipLaunchKernelGGL(colsum_kn_kernel, dim3(cdiv(d->N, 64)), dim3(256), 0, s, a.B, d->K, d->N, d->ldb, d->alpha,
+        ERGM_LAUNCH(colsum_kn_kernel, dim3(cdiv(d->N, 64)), dim3(256), 0, s, a.B, d->K, d->N, d->ldb, d->alpha,
                            d->alpha_dev, d->bias_grad);
     return check_launch("ergm_gemm");
 }
@@ -1440,7 +1440,7 @@ static void launch_dw2_cfg(const GemmArgs2& g, int nblocks, hipStream_t s) {
     auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il>;
     static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
     (void)attr;
-    hipLaunchKernelGGL(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
+    ERGM_LAUNCH(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
 }
 
 // Two weight-gradient GEMMs (a_layout KM, b_layout KN, epilogue NONE, f32 C) in one launch when both plan

@@ -173,6 +173,10 @@ struct ergm_model_plan {
     // (and the stacked caption K/V GEMM in forward), forked/joined with events.
     hipStream_t side;
     hipEvent_t ev_fork;
+    // fork points bound to the producing launch (common.h ERGM_LAUNCH; ERGM_BIND_FORKS=0: hipEventRecord)
+    bool bind_forks = true;
+    hipEvent_t pt_ev = nullptr;  // the last fork point taken on pt_s, reusable while nothing is launched there
+    hipStream_t pt_s = nullptr;
     std::vector<hipEvent_t> ev_join;  // one per backward stage (L layers + head + embed)
     // inputs
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
@@ -417,15 +421,45 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
 }
 
 
+// Executor streams.  ERGM_<NAME>_CUMASK (hex, most significant digit first, bit i = logical CU i) creates the
+// stream with a CU mask (hipExtStreamCreateWithCUMask) — for experiments that keep stream classes on disjoint CUs.
+hipError_t make_stream(hipStream_t* s, const char* env) {
+    const char* m = getenv(env);
+    if (!m || !*m) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    std::vector<uint32_t> mask;
+    const size_t n = strlen(m);
+    for (size_t end = n; end > 0;) {  // 8 hex digits per word, least significant word first
+        const size_t beg = end >= 8 ? end - 8 : 0;
+        mask.push_back((uint32_t)strtoul(std::string(m + beg, end - beg).c_str(), nullptr, 16));
+        end = beg;
+    }
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 // Fork/join events order two streams of the same device: device-scope release is enough, and skipping
 // the system-scope fence avoids an L2 writeback at every record on the critical stream.
 constexpr unsigned kSyncEv = hipEventDisableTiming | hipEventDisableSystemFence;
 
+// An event that completes with everything enqueued so far on `s`: the fork point armed before the stage's last
+// launch on s when that launch carried it (arm_fork: no marker packet on s), else `ev` recorded on s.
+hipEvent_t stream_point(ergm_model_plan* P, hipStream_t s, hipEvent_t ev) {
+    hipEvent_t e = bind_take(s);
+    if (!e && hipEventRecord(ev, s) == hipSuccess) e = ev;
+    P->pt_ev = e;
+    P->pt_s = s;
+    watch_stream(s);
+    return e;
+}
+// Bind the next fork point of `s` to the launches that follow on s (the stage's producer of the fork).
+void arm_fork(ergm_model_plan* P, hipStream_t s) {
+    if (!P->dry && P->bind_forks) bind_arm(s, P->ev_fork);
+}
+
 // Make the side stream wait for everything issued so far on `s` (the producer of a dW GEMM's dY).
 int fork_side(ergm_model_plan* P, hipStream_t s) {
     if (P->dry) return ERGM_OK;
-    if (hipEventRecord(P->ev_fork, s) != hipSuccess || hipStreamWaitEvent(P->side, P->ev_fork, 0) != hipSuccess)
-        return fail(ERGM_EHIP, "model: stream fork failed");
+    hipEvent_t e = stream_point(P, s, P->ev_fork);
+    if (!e || hipStreamWaitEvent(P->side, e, 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream fork failed");
     return ERGM_OK;
 }
 
@@ -691,7 +725,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->side = nullptr;
     P->ev_fork = nullptr;
     P->ev_join.assign(d.n_layer + 3, nullptr);
-    bool ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess &&
+    bool ok = make_stream(&P->side, "ERGM_SIDE_CUMASK") == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     // forward chains over batch slices (1..4; ERGM_FWD_CHAINS, A/B measurements)
@@ -705,6 +739,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_DW_MAIN")) P->dw_main = atoi(e);
     P->dw_batch = true;
     if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
+    if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -715,7 +750,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->per_stage_join = true;
     P->fwd2 = nullptr;
     for (auto& e : P->ev_f2) e = nullptr;
-    ok = ok && hipStreamCreateWithFlags(&P->fwd2, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && make_stream(&P->fwd2, "ERGM_FWD2_CUMASK") == hipSuccess;
     for (auto& e : P->ev_f2) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     for (int c = 0; c < 2; ++c) {
         P->fwdx[c] = nullptr;
@@ -1287,7 +1322,11 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     auto Tc = [&](int c) { return ch.nb[c] * S; };
     auto lnrow = [&](const float* p, int c) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S; };
     // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
+    // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
+    // fork's event itself (arm_fork before it) instead of a marker packet recorded behind it
+    const bool arm = ch.n == 1 && !P->dry;
     ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
+    if (arm) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
                       R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
@@ -1304,6 +1343,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (arm && !P->capkv_split) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
         if (!P->dry) {
             const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
             __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1343,6 +1383,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (arm) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
         if (!P->dry) {
             const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
             const size_t bhs = (size_t)ch.b0[c] * H * S;
@@ -1358,6 +1399,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
                       ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l, LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B)));
@@ -1440,7 +1482,7 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
                        "model_set_optimizer: range %d must be non-empty, 4-element aligned", k);
     ERGM_CHECK_ARG(o->wte_begin >= 0 && o->wte_begin % 4 == 0, "model_set_optimizer: bad wte_begin");
     if (!P->opt_s) {
-        if (hipStreamCreateWithFlags(&P->opt_s, hipStreamNonBlocking) != hipSuccess)
+        if (make_stream(&P->opt_s, "ERGM_OPT_CUMASK") != hipSuccess)
             return fail(ERGM_EHIP, "model_set_optimizer: stream creation");
         P->ev_opt.assign(L + 4, nullptr);
         for (auto& e : P->ev_opt)
@@ -1462,7 +1504,10 @@ namespace {
 // side stream, for the side stream's weight-gradient mark `mark` (< 0: none).
 int opt_wait(ergm_model_plan* P, hipStream_t s, int mark) {
     hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
-    if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
+    // the stage's last fork point, when nothing was launched (or joined) on s since it was taken
+    const bool reuse = P->pt_ev && P->pt_s == s && g_watch_s == s && !g_watch_dirty && !P->per_stage_join;
+    if (reuse) e = P->pt_ev;
+    if ((!reuse && hipEventRecord(e, s) != hipSuccess) || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
         return fail(ERGM_EHIP, "model: optimizer stream wait");
     if (mark >= 0 && hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) != hipSuccess)
         return fail(ERGM_EHIP, "model: optimizer stream wait");

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
                                                      float* __restrict__ part_b, int rows, int E, DropSite drop,
                                                      int drop_res) {
-    __shared__ float red[2][LN_WAVES_BWD][NV * 256];
+    __shared__ float red[LN_WAVES_BWD][NV * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 pg[NV], pb[NV], gm[NV];
 #pragma unroll
@@ -188,23 +188,25 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
             }
         }
     }
-    // cross-wave reduction of the partial column sums (fixed order → deterministic)
+    // cross-wave reduction of the partial column sums (fixed order → deterministic): dγ then dβ through one
+    // [waves][E] buffer, so the workgroup holds 24 KB of LDS (at E = 768) and fits beside the GEMM tiles of the
+    // concurrent weight-gradient stream
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int c = (i * 64 + lane) * 4;
-        *reinterpret_cast<float4*>(&red[0][wave][c]) = pg[i];
-        *reinterpret_cast<float4*>(&red[1][wave][c]) = pb[i];
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < E; c += 64 * LN_WAVES_BWD) {
-        float a = red[0][0][c], b = red[1][0][c];
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();  // dγ's reads of the buffer are done
 #pragma unroll
-        for (int w = 1; w < LN_WAVES_BWD; ++w) {
-            a += red[0][w][c];
-            b += red[1][w][c];
+        for (int i = 0; i < NV; ++i) {
+            int c = (i * 64 + lane) * 4;
+            *reinterpret_cast<float4*>(&red[wave][c]) = h ? pb[i] : pg[i];
         }
-        part_g[(size_t)blockIdx.x * E + c] = a;
-        part_b[(size_t)blockIdx.x * E + c] = b;
+        __syncthreads();
+        float* out = h ? part_b : part_g;
+        for (int c = threadIdx.x; c < E; c += 64 * LN_WAVES_BWD) {
+            float a = red[0][c];
+#pragma unroll
+            for (int w = 1; w < LN_WAVES_BWD; ++w) a += red[w][c];
+            out[(size_t)blockIdx.x * E + c] = a;
+        }
     }
 }
 
@@ -321,13 +323,13 @@ int colsum_impl(const void* X, bool bf16_in, int rows, int cols, int ldx, float*
         ERGM_CHECK_ARG(ws && ws_bytes >= need, "colsum: workspace %zu < %zu", ws_bytes, need);
     }
     if (bf16_in)
-        hipLaunchKernelGGL(colsum_partial_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
+        ERGM_LAUNCH(colsum_partial_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
                            (int)direct);
     else
-        hipLaunchKernelGGL(colsum_partial_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
+        ERGM_LAUNCH(colsum_partial_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ldx, ws, out, accumulate,
                            (int)direct);
     if (!direct)
-        hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, s, ws, nparts, cols, out,
+        ERGM_LAUNCH(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, s, ws, nparts, cols, out,
                            accumulate);
     return check_launch("colsum");
 }
@@ -354,10 +356,10 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
     int nv = cdiv(E, 256);
     auto* yb = reinterpret_cast<__bf16*>(y);
     switch (nv) {
-        case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 1: ERGM_LAUNCH(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 2: ERGM_LAUNCH(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 3: ERGM_LAUNCH(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        default: ERGM_LAUNCH(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
     }
     return check_launch("layernorm_fwd");
 }
@@ -375,7 +377,7 @@ __global__ void ones_col_kernel(__bf16* p, int rows, int ld, int col) {
 
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s) {
     ERGM_CHECK_ARG(p && rows > 0 && col % 8 == 0 && ld >= col + 8, "fill_ones_col: bad argument");
-    hipLaunchKernelGGL(ones_col_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, s, reinterpret_cast<__bf16*>(p), rows, ld,
+    ERGM_LAUNCH(ones_col_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, s, reinterpret_cast<__bf16*>(p), rows, ld,
                        col);
     return check_launch("fill_ones_col");
 }
@@ -406,10 +408,10 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     switch (cdiv(E, 256)) {
-        case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 1: ERGM_LAUNCH(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 2: ERGM_LAUNCH(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 3: ERGM_LAUNCH(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        default: ERGM_LAUNCH(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
     }
     return check_launch("layernorm_bwd");
 }
@@ -422,7 +424,7 @@ int layernorm_param_reduce_n(int n, const float* const* part_g, const float* con
         ERGM_CHECK_ARG(part_g[i] && part_b[i] && dgamma[i] && dbeta[i], "layernorm_param_reduce: null argument");
         j.part_g[i] = part_g[i]; j.part_b[i] = part_b[i]; j.dgamma[i] = dgamma[i]; j.dbeta[i] = dbeta[i];
     }
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(E, 32), 2, n), dim3(256), 0, s, j, ln_bwd_nparts(rows), E);
+    ERGM_LAUNCH(ln_param_reduce_kernel, dim3(cdiv(E, 32), 2, n), dim3(256), 0, s, j, ln_bwd_nparts(rows), E);
     return check_launch("layernorm_param_reduce");
 }
 

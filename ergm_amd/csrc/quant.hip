@@ -211,8 +211,8 @@ int quant_weights_fp8(const WqJobs& J0, hipStream_t s) {
         ba += cdiv(j.N, WQ_AMAX_COLS) * cdiv(j.K, WQ_AMAX_ROWS);
         bq += (j.N / 64) * (j.K / 64);
     }
-    hipLaunchKernelGGL(wq_amax_kernel, dim3(ba), dim3(256), 0, s, J);
-    hipLaunchKernelGGL(wq_quant_kernel, dim3(bq), dim3(256), 0, s, J);
+    ERGM_LAUNCH(wq_amax_kernel, dim3(ba), dim3(256), 0, s, J);
+    ERGM_LAUNCH(wq_quant_kernel, dim3(bq), dim3(256), 0, s, J);
     return check_launch("quant_weights_fp8");
 }
 
@@ -226,12 +226,12 @@ int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void
     auto* q = reinterpret_cast<uint8_t*>(Q);
     const int nch = cdiv(cols, 512);
     if (x_dtype == ERGM_BF16) {
-        if (nch <= 2) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 2>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
-        else if (nch <= 4) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 4>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
-        else if (nch <= 8) hipLaunchKernelGGL((quant_rows_reg_kernel<true, 8>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
-        else hipLaunchKernelGGL(quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        if (nch <= 2) ERGM_LAUNCH((quant_rows_reg_kernel<true, 2>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else if (nch <= 4) ERGM_LAUNCH((quant_rows_reg_kernel<true, 4>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else if (nch <= 8) ERGM_LAUNCH((quant_rows_reg_kernel<true, 8>), grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        else ERGM_LAUNCH(quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
     } else {
-        hipLaunchKernelGGL(quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
+        ERGM_LAUNCH(quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, scale);
     }
     return check_launch("quant_rows_fp8");
 }

@@ -148,6 +148,9 @@ __global__ __launch_bounds__(256) void count_valid_kernel(const int64_t* __restr
 // dh[b,S-1,:] += dlogits[b]·W.  CrossEntropyLoss semantics (src/model.py:710-711): labels outside
 // [0, C) (-100 = ignore_index) contribute neither loss nor gradient; the mean is over the n_valid
 // (global) valid labels.
+// Latency-bound (B workgroups, a few KB each): every global load of a phase is issued before the first use, so
+// the phase pays one memory latency instead of one per loop iteration; the sums keep the lane-strided order.
+constexpr int EMO_EV = 16;  // E <= 64 * EMO_EV (the LayerNorm kernels' limit, 1024)
 __global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restrict__ h, const float* __restrict__ W,
                                                           const int64_t* __restrict__ labels, float* __restrict__ logits,
                                                           float* __restrict__ scratch, float* __restrict__ dh, int B, int S,
@@ -157,10 +160,18 @@ __global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restri
     const int b = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const __bf16* hr = h + ((size_t)b * S + S - 1) * E;
+    float hv[EMO_EV];
+#pragma unroll
+    for (int k = 0; k < EMO_EV; ++k) hv[k] = lane + 64 * k < E ? bf2f(hr[lane + 64 * k]) : 0.f;
     for (int c = wave; c < C; c += 4) {
         const float* wr = W + (size_t)c * E;
+        float wv[EMO_EV];
+#pragma unroll
+        for (int k = 0; k < EMO_EV; ++k) wv[k] = lane + 64 * k < E ? wr[lane + 64 * k] : 0.f;
         float acc = 0.f;
-        for (int e = lane; e < E; e += 64) acc += bf2f(hr[e]) * wr[e];
+#pragma unroll
+        for (int k = 0; k < EMO_EV; ++k)
+            if (lane + 64 * k < E) acc += hv[k] * wv[k];
         acc = wave_sum(acc);
         if (lane == 0) {
             lg[c] = acc;
@@ -187,14 +198,30 @@ __global__ __launch_bounds__(256) void emotion_row_kernel(const __bf16* __restri
     }
     __syncthreads();
     if (!dh) return;
-    for (int e = threadIdx.x; e < E; e += 256) {
+    float* dr = dh + ((size_t)b * S + S - 1) * E;
+    constexpr int EPT = EMO_EV / 4;  // columns per thread (256 threads)
+    float wv[EPT][16], o[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        o[k] = e < E ? dr[e] : 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) wv[k][c] = (c < C && e < E) ? W[(size_t)c * E + e] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        if (e >= E) continue;
         float acc = 0.f;
-        for (int c = 0; c < C; ++c) acc += dl[c] * W[(size_t)c * E + e];
-        dh[((size_t)b * S + S - 1) * E + e] += acc;
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            if (c < C) acc += dl[c] * wv[k][c];
+        dr[e] = o[k] + acc;
     }
 }
 
-// dW[c][e] = Σ_b dlogits[b][c]·h[b,S-1,e] (fixed b order); block 0 also sums the row losses.
+// dW[c][e] = Σ_b dlogits[b][c]·h[b,S-1,e] (fixed b order); block 0 also sums the row losses.  The dlogits are
+// staged in LDS and the h column of 16 samples is loaded at once, so a chunk pays one memory latency.
 __global__ __launch_bounds__(256) void emotion_dw_kernel(const __bf16* __restrict__ h, const float* __restrict__ scratch,
                                                          float* __restrict__ loss_sum, float* __restrict__ dW, int B,
                                                          int S, int E, int C) {
@@ -204,17 +231,31 @@ __global__ __launch_bounds__(256) void emotion_dw_kernel(const __bf16* __restric
         *loss_sum = s;
     }
     if (!dW) return;
+    __shared__ float dl[16][16];
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= E) return;
     float acc[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) acc[c] = 0.f;
-    for (int b = 0; b < B; ++b) {
-        float hv = bf2f(h[((size_t)b * S + S - 1) * E + e]);
+    for (int b0 = 0; b0 < B; b0 += 16) {
+        __syncthreads();
+        {
+            const int bb = threadIdx.x >> 4, c = threadIdx.x & 15;
+            dl[bb][c] = (b0 + bb < B && c < C) ? scratch[(size_t)(b0 + bb) * C + c] : 0.f;
+        }
+        float hv[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-            if (c < C) acc[c] += scratch[(size_t)b * C + c] * hv;
+        for (int j = 0; j < 16; ++j)
+            hv[j] = (e < E && b0 + j < B) ? bf2f(h[((size_t)(b0 + j) * S + S - 1) * E + e]) : 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (b0 + j >= B) break;
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                if (c < C) acc[c] += dl[j][c] * hv[j];
+        }
     }
+    if (e >= E) return;
 #pragma unroll
     for (int c = 0; c < 16; ++c)
         if (c < C) dW[(size_t)c * E + e] = acc[c];
@@ -280,7 +321,7 @@ using namespace ergm;
 extern "C" int ergm_count_valid(const int64_t* labels, const int64_t* emotion_labels, int B, int S, int V, int C,
                                 int* counts, void* stream) {
     ERGM_CHECK_ARG(counts && B > 0 && S > 0 && V > 0 && C > 0, "count_valid: bad argument");
-    hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, as_stream(stream), labels, emotion_labels, B, S, V, C,
+    ERGM_LAUNCH(count_valid_kernel, dim3(1), dim3(256), 0, as_stream(stream), labels, emotion_labels, B, S, V, C,
                        counts);
     return check_launch("count_valid");
 }
@@ -297,11 +338,11 @@ extern "C" int ergm_xent_fwd_bwd(const void* logits, int ldl, const int64_t* lab
     auto* dl = reinterpret_cast<__bf16*>(dlogits);
     hipStream_t s = as_stream(stream);
     dim3 grid(B * S), blk(XE_THREADS);
-    if (nch <= 2) hipLaunchKernelGGL(xent_kernel<2>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
-    else if (nch <= 4) hipLaunchKernelGGL(xent_kernel<4>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
-    else if (nch <= 8) hipLaunchKernelGGL(xent_kernel<8>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
-    else if (nch <= 13) hipLaunchKernelGGL(xent_kernel<13>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
-    else hipLaunchKernelGGL(xent_kernel<16>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    if (nch <= 2) ERGM_LAUNCH(xent_kernel<2>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 4) ERGM_LAUNCH(xent_kernel<4>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 8) ERGM_LAUNCH(xent_kernel<8>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else if (nch <= 13) ERGM_LAUNCH(xent_kernel<13>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
+    else ERGM_LAUNCH(xent_kernel<16>, grid, blk, 0, s, lg, ldl, labels, n_valid_global, row_loss, dl, S, V);
     return check_launch("xent");
 }
 
@@ -309,16 +350,16 @@ extern "C" int ergm_emotion_head(const void* h, const float* W, const int64_t* l
                                  float* dW, float* dh, float* scratch, int B, int S, int E, int C,
                                  const int* n_valid_global, const float* grad_scale_dev, void* stream) {
     ERGM_CHECK_ARG(h && W && logits, "emotion_head: null argument");
-    ERGM_CHECK_ARG(B > 0 && C > 0 && C <= 16 && E > 0 && S > 0, "emotion_head: bad shape");
+    ERGM_CHECK_ARG(B > 0 && C > 0 && C <= 16 && E > 0 && E <= 64 * EMO_EV && S > 0, "emotion_head: bad shape");
     ERGM_CHECK_ARG(!labels || (loss_sum && scratch && n_valid_global), "emotion_head: labels need loss_sum, scratch and n_valid");
     ERGM_CHECK_ARG((dW == nullptr) == (dh == nullptr), "emotion_head: dW and dh go together");
     ERGM_CHECK_ARG(!dW || labels, "emotion_head: gradients need labels");
     hipStream_t s = as_stream(stream);
     const __bf16* hb = reinterpret_cast<const __bf16*>(h);
-    hipLaunchKernelGGL(emotion_row_kernel, dim3(B), dim3(256), 0, s, hb, W, labels, logits, scratch, dh, B, S, E, C,
+    ERGM_LAUNCH(emotion_row_kernel, dim3(B), dim3(256), 0, s, hb, W, labels, logits, scratch, dh, B, S, E, C,
                        n_valid_global, grad_scale_dev);
     if (labels)
-        hipLaunchKernelGGL(emotion_dw_kernel, dim3(dW ? cdiv(E, 256) : 1), dim3(256), 0, s, hb, scratch, loss_sum, dW,
+        ERGM_LAUNCH(emotion_dw_kernel, dim3(dW ? cdiv(E, 256) : 1), dim3(256), 0, s, hb, scratch, loss_sum, dW,
                            B, S, E, C);
     return check_launch("emotion_head");
 }
@@ -327,7 +368,7 @@ extern "C" int ergm_loss_finalize(const float* row_loss, int T, const int* n_val
                                   const int* n_valid_emo, float* out, void* stream) {
     ERGM_CHECK_ARG(row_loss && out && T > 0, "loss_finalize: bad argument");
     ERGM_CHECK_ARG(!emo_loss_sum || n_valid_emo, "loss_finalize: the emotion loss needs its valid count");
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, as_stream(stream), row_loss, T, n_valid_global,
+    ERGM_LAUNCH(loss_finalize_kernel, dim3(1), dim3(256), 0, as_stream(stream), row_loss, T, n_valid_global,
                        emo_loss_sum, n_valid_emo, out, MetricAcc{});
     return check_launch("loss_finalize");
 }
@@ -350,7 +391,7 @@ int dlogits_add(void* dl, const void* g, const float* scale, size_t n, hipStream
     ERGM_CHECK_ARG(dl && g && n % 8 == 0 && aligned16(dl) && aligned16(g), "dlogits_add: bad argument");
     const size_t n8 = n / 8;
     const unsigned grid = (unsigned)std::min<size_t>((n8 + 255) / 256, 4096);
-    hipLaunchKernelGGL(dlogits_add_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<bf16x8*>(dl),
+    ERGM_LAUNCH(dlogits_add_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<bf16x8*>(dl),
                        reinterpret_cast<const bf16x8*>(g), scale, n8);
     return check_launch("dlogits_add");
 }
@@ -360,7 +401,7 @@ int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_globa
                           const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
                           const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s) {
     MetricAcc acc{loss_acc, reinterpret_cast<unsigned long long*>(correct), emo_logits, emo_labels, B, C};
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, row_loss, T, n_valid_global, emo_loss_sum,
+    ERGM_LAUNCH(loss_finalize_kernel, dim3(1), dim3(256), 0, s, row_loss, T, n_valid_global, emo_loss_sum,
                        n_valid_emo, out, acc);
     return check_launch("loss_finalize");
 }
