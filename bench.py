@@ -224,6 +224,8 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if os.environ.get("ERGM_MAIN_PRIO"):  # experiment hook: the step on a stream of the given priority (-1 high)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=int(os.environ["ERGM_MAIN_PRIO"])))
     if os.environ.get("ERGM_MAIN_CUMASK"):  # experiment hook: the caller's stream restricted to a CU mask
         import ctypes as C
         from ergm_amd import _lib

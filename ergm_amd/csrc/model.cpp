@@ -137,6 +137,11 @@ struct ergm_model_plan {
     // cost more there than the two large ones at the end, where they overlap the optimizer tail
     int capkv_split = 0;
     int opt_lag = 2;  // ERGM_OPT_LAG: stages between a block's backward and its AdamW launch (opt_after_layer)
+    // ERGM_DW_SHIFT=1: the weight-gradient pairs are launched when their SECOND member's dY is final, half a
+    // sub-block later than the default (c_fc + cross c_proj after ln_2's backward, q + attn c_proj after ln_x's,
+    // c_attn + the next block's mlp c_proj after ln_1's), so the side stream has work while the attention
+    // backwards run alone on the data-gradient chain
+    bool dw_shift = false;
     std::vector<DwJob> dw_pend;
     bool bwd_forked;
     hipStream_t fwd2;
@@ -425,6 +430,10 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
 // stream with a CU mask (hipExtStreamCreateWithCUMask) — for experiments that keep stream classes on disjoint CUs.
 hipError_t make_stream(hipStream_t* s, const char* env) {
     const char* m = getenv(env);
+    // ERGM_<NAME>_PRIO (same name with PRIO for CUMASK): the stream's scheduling priority (HIP: 0 low ... -1 high)
+    std::string pe(env);
+    pe.replace(pe.find("CUMASK"), 6, "PRIO");
+    if (const char* pv = getenv(pe.c_str())) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, atoi(pv));
     if (!m || !*m) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     std::vector<uint32_t> mask;
     const size_t n = strlen(m);
@@ -444,6 +453,8 @@ constexpr unsigned kSyncEv = hipEventDisableTiming | hipEventDisableSystemFence;
 // launch on s when that launch carried it (arm_fork: no marker packet on s), else `ev` recorded on s.
 hipEvent_t stream_point(ergm_model_plan* P, hipStream_t s, hipEvent_t ev) {
     hipEvent_t e = bind_take(s);
+    // the previous point of s, when nothing was launched (or joined) on s since it was taken
+    if (!e && P->pt_ev && P->pt_s == s && g_watch_s == s && !g_watch_dirty && !P->per_stage_join) e = P->pt_ev;
     if (!e && hipEventRecord(ev, s) == hipSuccess) e = ev;
     P->pt_ev = e;
     P->pt_s = s;
@@ -740,6 +751,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->dw_batch = true;
     if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
     if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
+    if (const char* e = getenv("ERGM_DW_SHIFT")) P->dw_shift = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -1185,14 +1197,23 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         const char* e = getenv("ERGM_FWD_INTERLEAVE");
         return !(e && e[0] == '0');
     }();
-    for (int l = 0; l < L; ++l) {
-        if (interleave && nchain > 1) {
-            for (int part = 0; part <= 10; ++part)
-                for (int c = 0; c < nchain; ++c)
-                    ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], part));
-        } else {
+    // ERGM_FWD_LAG = k: chain c is enqueued c·k launches behind chain 0 (the chains' kernel types then differ at
+    // any moment: one chain's GEMM beside the other's attention / LayerNorm)
+    static const int lag = [] {
+        const char* e = getenv("ERGM_FWD_LAG");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    constexpr int NP = 11;  // fwd_block parts
+    if (interleave && nchain > 1) {
+        for (int g = 0; g < L * NP + (nchain - 1) * lag; ++g)
+            for (int c = 0; c < nchain; ++c) {
+                const int gc = g - c * lag;
+                if (gc < 0 || gc >= L * NP) continue;
+                ERGM_TRY(fwd_block(P, gc / NP, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], gc % NP));
+            }
+    } else {
+        for (int l = 0; l < L; ++l)
             for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
-        }
     }
     for (int c = 1; c < nchain && !P->dry; ++c)
         if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
@@ -1325,25 +1346,29 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
     // fork's event itself (arm_fork before it) instead of a marker packet recorded behind it
     const bool arm = ch.n == 1 && !P->dry;
-    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
-    if (arm) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
+    const bool shift = P->dw_shift && !P->capkv_split && P->dw_batch;
+    if (!shift || l == L - 1)  // (shifted: block l's mlp c_proj dW was queued at the end of block l+1's stage)
+        ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
+    if (arm && !shift) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
                       R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
     ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), 2));
-    ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
+    if (!shift) ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (arm && shift) arm_fork(P, s);  // ln_2's backward: dh2, the cross c_proj dW's dY
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), 4));
+    if (shift) ERGM_TRY(dw_flush(P, ch));  // c_fc + cross c_proj (+ mlp c_proj in the first stage)
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm && !P->capkv_split) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
+        if (arm && !P->capkv_split && !shift) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
         if (!P->dry) {
             const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
             __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1371,19 +1396,21 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                           P->dry ? nullptr : reinterpret_cast<const __bf16*>(p.capkv_w_b) + co, L2E, ERGM_NK, R(P->dcap, c, E), E, ERGM_F32,
                           l == L - 1 ? ERGM_EPI_NONE : ERGM_EPI_ACCUM));
     }
-    ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q + caption K/V weight gradients
+    if (!shift) ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q + caption K/V weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (arm && shift) arm_fork(P, s);  // ln_x's backward: dh1, the attn c_proj dW's dY
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), 16));
+    if (shift) ERGM_TRY(dw_flush(P, ch));  // q + attn c_proj
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
+        if (arm && !shift) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
         if (!P->dry) {
             const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
             const size_t bhs = (size_t)ch.b0[c] * H * S;
@@ -1395,7 +1422,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
     }
     ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B), 32));
-    ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
+    if (!shift) ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c) {
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
                       ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
@@ -1403,6 +1430,14 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l, LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B)));
+    if (shift) {  // c_attn + the next stage's mlp c_proj (its dY is this stage's last output, dh0 = block l-1's dh3)
+        if (l > 0) {
+            const LayerActs an = P->dry ? LayerActs{} : P->la[l - 1];
+            ERGM_TRY(dw_gemm(P, ch, F, E, an.act, P->XF, dh0, E, LG(P, l - 1, ERGM_T_MPROJ_W),
+                             LG(P, l - 1, ERGM_T_MPROJ_B), 1));
+        }
+        ERGM_TRY(dw_flush(P, ch));
+    }
     (void)lnrow;
     // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
     // those of the block differentiated before, so block l+1's gradients are final on return.

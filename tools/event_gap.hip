@@ -20,8 +20,20 @@
 
 // producer: every workgroup spins ~`ns` then block 0 writes `val` to slot[i]
 __global__ void producer(unsigned* slot, int i, unsigned val, long long cycles, float4* dirty, int nd) {
-    for (int k = 0; k < nd; ++k)  // nd float4 per thread of dirty data (L2 write-back pressure at the fork)
-        dirty[((size_t)blockIdx.x * nd + k) * blockDim.x + threadIdx.x] = make_float4(val, k, 0, 0);
+    // nd float4 per thread of dirty data (L2 write-back pressure at the fork); nd >= 1000: nd-1000 float4 written
+    // with non-temporal stores; nd >= 2000: nd-2000 written through (sc1 buffer stores)
+    const int mode = nd >= 2000 ? 2 : nd >= 1000 ? 1 : 0;
+    const int n = nd - 1000 * mode;
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    typedef unsigned u4v __attribute__((__vector_size__(16)));
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(dirty, 0, 0x7fffffff, 0x00020000);
+    for (int k = 0; k < n; ++k) {
+        const size_t e = ((size_t)blockIdx.x * n + k) * blockDim.x + threadIdx.x;
+        const f4 v{(float)val, (float)k, 0.f, 0.f};
+        if (mode == 1) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(dirty + e));
+        else if (mode == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, (int)(e * 16), 0, 16);
+        else dirty[e] = make_float4(val, k, 0, 0);
+    }
     const long long t0 = clock64();
     while (clock64() - t0 < cycles) {
     }
@@ -48,7 +60,7 @@ int main() {
     hipEvent_t t0, t1;
     CK(hipEventCreate(&t0));
     CK(hipEventCreate(&t1));
-    for (int nd : {0, 16, 64})
+    for (int nd : {0, 64, 1064, 2064})
     for (int rep = 0; rep < 2; ++rep)
         for (int mode = 0; mode < 3; ++mode) {
             CK(hipMemset(slot, 0, N * 4));
