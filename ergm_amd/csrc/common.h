@@ -107,6 +107,19 @@ struct WqJobs {
     WqJob j[8];
     int n;
 };
+// MX-fp8 weight quantisation jobs (quant.hip): W [K][ldw] bf16 -> Wt [N][ldt] e4m3 (transposed) with an e8m0
+// scale per (column, 32-row block): sc [N][lds]
+struct MxJob {
+    const __bf16* W;
+    uint8_t* Wt;
+    uint8_t* sc;
+    int ldw, K, N, ldt, lds;
+    int blk;  // first block of this job in the grid (set by quant_weights_mx)
+};
+struct MxJobs {
+    MxJob j[8];
+    int n;
+};
 
 // wave-level reductions over 64 lanes, all VALU (no ds_bpermute round trips): DPP quad_perm [1,0,3,2]
 // and [2,3,0,1], row_half_mirror and row_mirror inside each 16-lane row, then the gfx950 row swaps
@@ -192,6 +205,42 @@ __device__ __forceinline__ unsigned drop_keep4(const DropSite& d, int64_t row, i
 // Single element (any col): the word col & 3 of its group.
 __device__ __forceinline__ bool drop_keep1(const DropSite& d, int64_t row, int col) {
     return (drop_keep4(d, row, col & ~3) >> (col & 3)) & 1u;
+}
+
+// ---- MX-fp8 (OCP microscaling) helpers: 32-element blocks, e8m0 block scale 2^(e-127), e4m3fn elements ----
+// Block exponent: the smallest e with amax <= 448·2^e (no element saturates), from the bits of amax: amax =
+// 1.f·2^ea gives e = ea - 8, or ea - 7 when 1.f > 1.75 (448 = 1.75·2^8).  A zero block gets e = 0 (scale 1).
+// Returned biased (e + 127, clamped to [0, 254]); the scaled values v·2^-e are exact in f32.
+__device__ __forceinline__ int mx_exp_biased(float amax) {
+    const uint32_t b = __float_as_uint(amax);
+    if (amax == 0.f) return 127;
+    const int ea = (int)((b >> 23) & 0xff) - 127;
+    const int e = ea - 8 + ((b & 0x7fffff) > 0x600000u ? 1 : 0);
+    return min(max(e + 127, 0), 254);
+}
+__device__ __forceinline__ float mx_inv_scale(int eb) { return __uint_as_float((uint32_t)(254 - eb) << 23); }  // 2^-(eb-127)
+__device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d) {
+    a = fminf(fmaxf(a, -448.f), 448.f);
+    b = fminf(fmaxf(b, -448.f), 448.f);
+    c = fminf(fmaxf(c, -448.f), 448.f);
+    d = fminf(fmaxf(d, -448.f), 448.f);
+    int q = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    q = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, q, true);
+    return (uint32_t)q;
+}
+// 8 consecutive values of a 32-element block held by 4 consecutive lanes (lane & 3 = position in the block):
+// block amax across the 4 lanes, then 8 e4m3 bytes; returns the biased block exponent
+__device__ __forceinline__ int mx_quant8_x4(const float* v, uint2& q) {
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[j]));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    const int eb = mx_exp_biased(am);
+    const float is = mx_inv_scale(eb);
+    q.x = mx_pack4(v[0] * is, v[1] * is, v[2] * is, v[3] * is);
+    q.y = mx_pack4(v[4] * is, v[5] * is, v[6] * is, v[7] * is);
+    return eb;
 }
 
 // Host: the descriptor of one site (p in [0, 1); p == 0 gives thresh 0 = off).

@@ -48,6 +48,14 @@ struct GemmArgs {
     float* colsum_part;    // split-K: per-split partial column sums [z][N] (combined by splitk_reduce_kernel)
     int xcd_split;         // split-K over 8 K slices, one per XCD: grid.x = 8·tiles, slice = blockIdx.x & 7, so
                            // every tile of one K slice shares an XCD's L2 (pipelined kernel only)
+    // MX-fp8 GEMM (gemm_mx_kernel): e8m0 scales of every 32-element K block, A [M][ld_sa], B [N][ld_sb] bytes
+    const uint8_t* a_mx;
+    const uint8_t* b_mx;
+    int ld_sa, ld_sb;
+    // MX-fp8 copy of the (bf16) output C written by the epilogue: q_out [M][ld_q] e4m3, q_sc [M][ld_qs] e8m0
+    uint8_t* q_out;
+    uint8_t* q_sc;
+    int ld_q, ld_qs;
 };
 
 template <int EPI, bool OUT_BF16>
@@ -114,7 +122,10 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
     if (OUT_BF16) {
         bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+        for (int j = 0; j < 8; ++j) {
+            o[j] = f2bf(v[j]);
+            v[j] = bf2f(o[j]);  // the stored value (an MX copy quantises exactly what the bf16 consumers read)
+        }
         bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(a.C) + idx);
         if (a.nt_store) __builtin_nontemporal_store(o, dst);
         else *dst = o;
@@ -141,7 +152,7 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
 // (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
 // the staging buffer is (BM/WGM)*(BN+4) floats.  slab != nullptr: raw f32 split-K partials.
 template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN,
-          bool RS = false>
+          bool RS = false, bool QMX = false>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
                                            float alpha, float* slab) {
     // NT: every thread of the workgroup (a warp-specialised kernel adds producer waves, which only
@@ -168,6 +179,26 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
         for (int c = threadIdx.x; c < WM * CPR; c += NT) {
             const int row = c / CPR, col = (c % CPR) * 8;
             const int m = m0 + pass * WM + row, n = n0 + col;
+            if constexpr (QMX) {  // every lane reaches the block's shuffles (WM·CPR is a multiple of NT here)
+                static_assert(BN % 32 == 0 && (WM * CPR) % NT == 0, "MX epilogue: whole 32-column blocks per pass");
+                const bool ok = m < a.M && n < a.N;
+                const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
+                const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
+                float v[8] = {x0.x * alpha, x0.y * alpha, x0.z * alpha, x0.w * alpha,
+                              x1.x * alpha, x1.y * alpha, x1.z * alpha, x1.w * alpha};
+                if (ok) epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
+                else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+                }
+                uint2 q;
+                const int eb = mx_quant8_x4(v, q);
+                if (ok) {
+                    *reinterpret_cast<uint2*>(a.q_out + (size_t)m * a.ld_q + n) = q;
+                    if ((c & 3) == 0) a.q_sc[(size_t)m * a.ld_qs + (n >> 5)] = (uint8_t)eb;
+                }
+                continue;
+            }
             if (m >= a.M || n >= a.N) continue;
             const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
             const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
@@ -713,6 +744,20 @@ __device__ __forceinline__ i32x8 frag_f8(const char* lds, int ro) {
     return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 }
 
+// MX operand fragment: the block-scaled 16x16x128 MFMA reads a lane's 8 dwords as K positions {16g..16g+15} (dwords
+// 0-3) and {64+16g..64+16g+15} (dwords 4-7), g = lane >> 4, and applies the scale of lane group G to K positions
+// [32G, 32G+32) (measured: tools/mx_debug2.py).  Reading 16-B chunks g and g+4 of the row makes those positions
+// the row's memory order, so lane group G's scale byte is that of the 128-deep step's 32-element block G.
+__device__ __forceinline__ i32x8 frag_mx(const char* lds, int ro) {
+    const int lane = threadIdx.x & 63;
+    const int row = ro + (lane & 15), g = lane >> 4;
+    const char* base = lds + row * 128;
+    const int sw = swz_row(row);
+    const uint4 lo = *reinterpret_cast<const uint4*>(base + ((g ^ sw) << 4));
+    const uint4 hi = *reinterpret_cast<const uint4*>(base + (((g + 4) ^ sw) << 4));
+    return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
 template <int BM, int BN, int WGM, int WGN, int NS, int EPI, bool OUT_BF16>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmArgs a) {
     constexpr int NW = WGM * WGN;
@@ -774,6 +819,100 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmArgs a) {
     float alpha = a.alpha;
     if (a.alpha_dev) alpha *= *a.alpha_dev;
     store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * NW, true>(a, smem, acc, m0, n0, alpha, nullptr);
+}
+
+// MX-fp8 GEMM (OCP microscaling, config 5's forward): A [M][K] and B [N][K] e4m3 bytes (k contiguous) with an
+// e8m0 scale per 32-element K block of every row of A (a_mx [M][ld_sa]) and of B (b_mx [N][ld_sb]), consumed
+// by the MFMA itself: v_mfma_scale_f32_16x16x128_f8f6f4 takes the 32 bytes a lane holds (row l&15, K block
+// l>>4 of the 128-deep step) with that lane's scale byte.  The scales of a stage (4 bytes per row: the 4
+// blocks of a 128-deep step) ride in the same LDS ring behind the operand tiles, filled by 4-byte-per-lane
+// LDS-DMA (one 64-row piece per wave-instruction; with more waves than pieces the spare waves re-issue piece
+// 0, identical bytes, so every wave issues the same count and the counted waits stay exact).  No
+// per-row / per-column dequantisation in the epilogue; QMX: the epilogue also writes an MX copy of its bf16
+// output (the next fp8 GEMM's A operand).
+template <int BM, int BN, int WGM, int WGN, int NS, int EPI, bool OUT_BF16, bool QMX>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_mx_kernel(GemmArgs a) {
+    constexpr int NW = WGM * WGN;
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+    constexpr int SC_BYTES = (BM + BN) * 4;
+    constexpr int STAGE = A_BYTES + B_BYTES + SC_BYTES;
+    constexpr int NSP = (BM + BN) / 64;                // scale pieces per stage (64 rows each)
+    constexpr int SPW = (NSP + NW - 1) / NW;           // per wave
+    constexpr int LPS = GldsTile<BM, false, NW>::PER_WAVE + GldsTile<BN, false, NW>::PER_WAVE + SPW;
+    static_assert(NS >= 2 && NS <= 8 && (NS - 2) * LPS <= 63, "2..8 stages, vmcnt <= 63");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int nwg = a.tiles_m * a.tiles_n;
+    const int id = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    if (a.sweep_m) { tm = id % a.tiles_m; tn = id / a.tiles_m; }
+    else { tn = id % a.tiles_n; tm = id / a.tiles_n; }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int nk = a.K / 128;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / WGN, wn = wave % WGN;
+    const __bf16* A2 = a.A;
+    const __bf16* B2 = a.B;
+    const int lda2 = a.lda / 2, ldb2 = a.ldb / 2;
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_stage = [&](int kt) {
+        char* st = smem + (kt % NS) * STAGE;
+        const int k0 = kt * 64;
+        GldsTile<BM, false, NW>::issue(st, A2, lda2, m0, a.M, k0, wave);
+        GldsTile<BN, false, NW>::issue(st + A_BYTES, B2, ldb2, n0, a.N, k0, wave);
+#pragma unroll
+        for (int i = 0; i < SPW; ++i) {
+            int p = wave + i * NW;
+            if (p >= NSP) p = 0;  // spare wave: re-issue piece 0 (same bytes, same destination)
+            const bool isb = p * 64 >= BM;
+            const int r = (isb ? p * 64 - BM : p * 64) + lane;
+            const uint8_t* src = isb ? a.b_mx + (size_t)min(n0 + r, a.N - 1) * a.ld_sb + kt * 4
+                                     : a.a_mx + (size_t)min(m0 + r, a.M - 1) * a.ld_sa + kt * 4;
+            glds4(src, __builtin_amdgcn_readfirstlane(lds_addr_of(st + A_BYTES + B_BYTES + p * 256)));
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue_stage(s);
+    const int g = lane >> 4, r16 = lane & 15;
+    for (int kt = 0; kt < nk; ++kt) {
+        wait_stages<LPS, NS - 2>(min(NS - 2, nk - 1 - kt));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < nk) issue_stage(kt + NS - 1);
+        const char* st = smem + (kt % NS) * STAGE;
+        const uint32_t* sc = reinterpret_cast<const uint32_t*>(st + A_BYTES + B_BYTES);
+        i32x8 fa[FM], fb[FN];
+        int sa[FM], sb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            fa[i] = frag_mx(st, wm * WM + i * 16);
+            sa[i] = (int)(sc[wm * WM + i * 16 + r16] >> (8 * g));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            fb[j] = frag_mx(st + A_BYTES, wn * WN + j * 16);
+            sb[j] = (int)(sc[BM + wn * WN + j * 16 + r16] >> (8 * g));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0, 0, sa[i], 0,
+                                                                              sb[j]);
+    }
+    float alpha = a.alpha;
+    if (a.alpha_dev) alpha *= *a.alpha_dev;
+    store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * NW, false, QMX>(a, smem, acc, m0, n0, alpha, nullptr);
 }
 
 // split-K combine: C = epilogue(alpha * Σ_z slab[z]) in z order (deterministic).
@@ -1209,6 +1348,98 @@ static int plan_f8(int M, int N) {
 }
 
 }  // namespace ergm
+
+namespace ergm {
+template <int C, int EPI, bool OB, bool QMX>
+static void launch_mx_cfg(const GemmArgs& a, hipStream_t s) {
+    constexpr F8Cfg c = kF8Cfgs[C];
+    constexpr size_t stage = (size_t)(c.bm + c.bn) * 132;  // operand bytes (128 per row) + scale bytes (4 per row)
+    constexpr size_t lds = std::max((size_t)c.ns * stage, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
+    auto k = gemm_mx_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, EPI, OB, QMX>;
+    static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
+    (void)attr;
+    ERGM_LAUNCH(k, dim3(a.tiles_m * a.tiles_n), dim3(64 * c.wgm * c.wgn), lds, s, a);
+}
+template <int EPI, bool OB, bool QMX>
+static void launch_mx(const GemmArgs& a, int cfg, hipStream_t s) {
+    switch (cfg) {
+        case 0: launch_mx_cfg<0, EPI, OB, QMX>(a, s); break;
+        case 1: launch_mx_cfg<1, EPI, OB, QMX>(a, s); break;
+        case 2: launch_mx_cfg<2, EPI, OB, QMX>(a, s); break;
+        case 3: launch_mx_cfg<3, EPI, OB, QMX>(a, s); break;
+        default: launch_mx_cfg<4, EPI, OB, QMX>(a, s); break;
+    }
+}
+}  // namespace ergm
+
+extern "C" int ergm_gemm_mx(const ergm_gemm_desc* d, const void* A, const void* a_scale, int ld_sa, const void* B,
+                            const void* b_scale, int ld_sb, void* C, void* q_out, void* q_scale, int ld_q, int ld_qs,
+                            void* stream) {
+    using namespace ergm;
+    ERGM_CHECK_ARG(d && A && B && C && a_scale && b_scale, "ergm_gemm_mx: null argument");
+    ERGM_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0 && d->K % 128 == 0, "ergm_gemm_mx: K=%d must be a multiple of 128",
+                   d->K);
+    ERGM_CHECK_ARG(d->a_layout == ERGM_MK && d->b_layout == ERGM_NK, "ergm_gemm_mx: A [M][K] and B [N][K] only");
+    ERGM_CHECK_ARG(d->lda >= d->K && d->ldb >= d->K && d->lda % 16 == 0 && d->ldb % 16 == 0,
+                   "ergm_gemm_mx: lda/ldb >= K, multiples of 16 bytes");
+    ERGM_CHECK_ARG(ld_sa >= d->K / 32 && ld_sb >= d->K / 32 && ld_sa % 4 == 0 && ld_sb % 4 == 0,
+                   "ergm_gemm_mx: scale rows >= K/32 bytes, multiples of 4");
+    ERGM_CHECK_ARG(aligned16(A) && aligned16(B) && (reinterpret_cast<uintptr_t>(a_scale) & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(b_scale) & 3) == 0,
+                   "ergm_gemm_mx: operand / scale alignment");
+    ERGM_CHECK_ARG(d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldc >= d->N, "ergm_gemm_mx: N, ldc multiples of 8");
+    ERGM_CHECK_ARG(d->c_dtype == ERGM_F32 || d->c_dtype == ERGM_BF16, "ergm_gemm_mx: bad c_dtype");
+    const int e = d->epilogue;
+    ERGM_CHECK_ARG((e == ERGM_EPI_NONE || e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) ? d->c_dtype == ERGM_BF16 ||
+                       e == ERGM_EPI_NONE
+                                                                                        : e == ERGM_EPI_BIAS_RESID &&
+                                                                                              d->c_dtype == ERGM_F32,
+                   "ergm_gemm_mx: epilogue %d with c_dtype %d not supported", e, d->c_dtype);
+    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_RESID || (d->aux && d->ld_aux % 8 == 0), "ergm_gemm_mx: residual needs aux");
+    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || (d->aux_out && d->ld_aux_out % 8 == 0), "ergm_gemm_mx: GELU needs aux_out");
+    ERGM_CHECK_ARG(!q_out || (q_scale && e == ERGM_EPI_BIAS_GELU && d->N % 32 == 0 && ld_q >= d->N && ld_q % 8 == 0 &&
+                              ld_qs >= d->N / 32),
+                   "ergm_gemm_mx: the MX copy of C needs the BIAS_GELU epilogue, N % 32 == 0 and its buffers");
+    const int cfg = plan_f8(d->M, d->N);
+    GemmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = reinterpret_cast<const __bf16*>(A);
+    a.B = reinterpret_cast<const __bf16*>(B);
+    a.C = C;
+    a.M = d->M; a.N = d->N; a.K = d->K;
+    a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+    a.alpha = d->alpha; a.alpha_dev = d->alpha_dev;
+    a.bias = d->bias; a.aux = d->aux; a.ld_aux = d->ld_aux;
+    a.aux_out = d->aux_out; a.ld_aux_out = d->ld_aux_out;
+    a.tiles_m = cdiv(d->M, kF8Cfgs[cfg].bm);
+    a.tiles_n = cdiv(d->N, kF8Cfgs[cfg].bn);
+    a.sweep_m = (long)d->M < (long)d->N ? 1 : 0;
+    a.a_mx = reinterpret_cast<const uint8_t*>(a_scale);
+    a.b_mx = reinterpret_cast<const uint8_t*>(b_scale);
+    a.ld_sa = ld_sa; a.ld_sb = ld_sb;
+    a.q_out = reinterpret_cast<uint8_t*>(q_out);
+    a.q_sc = reinterpret_cast<uint8_t*>(q_scale);
+    a.ld_q = ld_q; a.ld_qs = ld_qs;
+    ERGM_TRY(check_dropout(d->dropout));
+    ERGM_CHECK_ARG(!d->dropout || d->dropout->p == 0.f || e == ERGM_EPI_BIAS_RESID,
+                   "ergm_gemm_mx: dropout applies to the BIAS_RESID epilogue only");
+    a.drop = drop_site_of(d->dropout, d->N);
+    hipStream_t s = as_stream(stream);
+    const bool ob = d->c_dtype == ERGM_BF16;
+    switch (e) {
+        case ERGM_EPI_NONE:
+            if (ob) launch_mx<ERGM_EPI_NONE, true, false>(a, cfg, s);
+            else launch_mx<ERGM_EPI_NONE, false, false>(a, cfg, s);
+            break;
+        case ERGM_EPI_BIAS: launch_mx<ERGM_EPI_BIAS, true, false>(a, cfg, s); break;
+        case ERGM_EPI_BIAS_GELU:
+            if (q_out) launch_mx<ERGM_EPI_BIAS_GELU, true, true>(a, cfg, s);
+            else launch_mx<ERGM_EPI_BIAS_GELU, true, false>(a, cfg, s);
+            break;
+        default: launch_mx<ERGM_EPI_BIAS_RESID, false, false>(a, cfg, s); break;
+    }
+    return check_launch("ergm_gemm_mx");
+}
 
 extern "C" int ergm_gemm_f8_tune(int cfg) {
     ERGM_CHECK_ARG(cfg >= -1 && cfg < ergm::kNumF8Cfgs, "gemm_f8_tune: cfg in [-1, %d)", ergm::kNumF8Cfgs);

@@ -26,8 +26,12 @@ using namespace ergm;
 
 namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
-                     int rows, int E, float eps, hipStream_t s, void* yq = nullptr, int ldq = 0, float* qscale = nullptr);
+                     int rows, int E, float eps, hipStream_t s, void* yq = nullptr, int ldq = 0, float* qscale = nullptr,
+                     void* qmx = nullptr, int ld_qmx = 0);
 int quant_weights_fp8(const WqJobs& J, hipStream_t s);
+int quant_weights_mx(const MxJobs& J, hipStream_t s);
+int quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
+                  hipStream_t s);
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
                    hipStream_t s);
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
@@ -69,6 +73,7 @@ struct LayerActs {
 struct LayerW8 {
     uint8_t* w[6];
     float* sc[6];
+    uint8_t* sx[6];  // MX-fp8: e8m0 scale per (column, 32-row block), [N][K/32]
     unsigned* amax;
     int amax_n;
 };
@@ -115,9 +120,14 @@ struct ergm_model_plan {
     // (ev_wq[l] marks block l's), the caption K/V weights likewise, and the transient row-quantised
     // activations (main stream: one buffer reused block after block; side stream: the captions)
     bool f8;
+    // MX-fp8 (default; ERGM_FP8_MX=0: the per-row / per-column scales): e8m0 scales per 32-element K block of
+    // every activation row and weight column, consumed by the MFMA (ergm_gemm_mx); the LayerNorms and the c_fc
+    // GELU epilogue write their MX copies themselves, the weights are quantised in one pass (no amax pass)
+    bool mx = true;
     std::vector<LayerW8> w8;
     uint8_t *capkv8, *qa, *qf, *qcap;
     float *capkv8_s, *sa, *sf, *scap;
+    uint8_t *capkv8_x, *xa, *xf, *xcap;
     unsigned* capkv_amax;
     std::vector<hipEvent_t> ev_wq;
     // per_stage_join: the caller's stream waits for block l+1's side-stream weight gradients at the end
@@ -275,6 +285,7 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->w8.assign(P->f8 ? L : 0, LayerW8{});
     P->capkv8 = P->qa = P->qf = P->qcap = nullptr;
     P->capkv8_s = P->sa = P->sf = P->scap = nullptr;
+    P->capkv8_x = P->xa = P->xf = P->xcap = nullptr;
     P->capkv_amax = nullptr;
     if (P->f8) {
         const size_t KN[6][2] = {{E, 3 * E}, {E, E}, {E, E}, {E, E}, {E, F}, {F, E}};
@@ -284,6 +295,7 @@ size_t carve(ergm_model_plan* P, char* base) {
             for (int i = 0; i < 6; ++i) {
                 w.w[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
                 w.sc[i] = c.take<float>(KN[i][1]);
+                w.sx[i] = c.take<uint8_t>(KN[i][0] / 32 * KN[i][1]);
                 na += (int)KN[i][1];
             }
             w.amax = c.take<unsigned>(na);
@@ -298,6 +310,10 @@ size_t carve(ergm_model_plan* P, char* base) {
         P->sf = c.take<float>(T);
         P->qcap = c.take<uint8_t>(T * E);
         P->scap = c.take<float>(T);
+        P->capkv8_x = c.take<uint8_t>((size_t)2 * E * L * (E / 32));
+        P->xa = c.take<uint8_t>(T * (E / 32));
+        P->xf = c.take<uint8_t>(T * (F / 32));
+        P->xcap = c.take<uint8_t>(T * (E / 32));
     }
     P->Fd = d.feat_dim > 0 ? d.feat_dim : (int)E;
     P->proj = d.has_features && P->Fd != (int)E;
@@ -412,9 +428,12 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
 }
 
 // fp8 forward GEMM: C[M][N] = epi(sa[m]·sb[n]·A8[m][:]·B8t[n][:]) (both operands k-contiguous, K bytes)
-int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* Bt,
-          const float* sb, void* C, int ldc, int cdt, int epi, const float* bias, const void* aux = nullptr,
-          int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0, const ergm_dropout* dropout = nullptr) {
+// MX (P->mx): the scales are the e8m0 block scales ax [M][K/32] / bx [N][K/32]; qo / qox (BIAS_GELU only): the MX
+// copy of the bf16 output [M][N] / [M][N/32] for the next fp8 GEMM.
+int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* ax,
+          const uint8_t* Bt, const float* sb, const uint8_t* bx, void* C, int ldc, int cdt, int epi, const float* bias,
+          const void* aux = nullptr, int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0,
+          const ergm_dropout* dropout = nullptr, uint8_t* qo = nullptr, uint8_t* qox = nullptr) {
     if (P->dry) return ERGM_OK;
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
@@ -422,7 +441,15 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
     g.a_layout = ERGM_MK; g.b_layout = ERGM_NK; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
     g.dropout = dropout;
+    if (P->mx) return ergm_gemm_mx(&g, A, ax, K / 32, Bt, bx, K / 32, C, qo, qox, N, N / 32, s);
     return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
+}
+// Row quantisation of an fp8 GEMM's activation operand (attention outputs, caption embeddings; the GELU output
+// too without MX): per-row scale `sf` or MX block scales `sx`.
+int quant_act(ergm_model_plan* P, const void* X, int ldx, int rows, int cols, uint8_t* q, float* sf, uint8_t* sx,
+              hipStream_t s) {
+    if (P->mx) return quant_rows_mx(X, ERGM_BF16, ldx, rows, cols, q, cols, sx, cols / 32, s);
+    return quant_rows_fp8(X, ERGM_BF16, ldx, rows, cols, q, cols, sf, s);
 }
 
 
@@ -652,9 +679,16 @@ int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
     if (P->dry) return ERGM_OK;
     const int E = P->d.n_embd, F = P->d.n_inner;
     LayerW8& w = P->w8[l];
-    if (hipMemsetAsync(w.amax, 0, (size_t)w.amax_n * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "model: memset");
     const int tens[6] = {ERGM_T_ATTN_W, ERGM_T_APROJ_W, ERGM_T_XQ_W, ERGM_T_XPROJ_W, ERGM_T_FC_W, ERGM_T_MPROJ_W};
     const int K[6] = {E, E, E, E, E, F}, N[6] = {3 * E, E, E, E, F, E};
+    if (P->mx) {  // one pass: block scales from each 32-row block's own maxima
+        MxJobs J{};
+        J.n = 6;
+        for (int i = 0; i < 6; ++i) J.j[i] = MxJob{LB(P, l, tens[i]), w.w[i], w.sx[i], N[i], K[i], N[i], K[i], K[i] / 32, 0};
+        ERGM_TRY(quant_weights_mx(J, ss));
+        return hipEventRecord(P->ev_wq[l], ss) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: event record");
+    }
+    if (hipMemsetAsync(w.amax, 0, (size_t)w.amax_n * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "model: memset");
     WqJobs J{};
     J.n = 6;
     unsigned* am = w.amax;
@@ -752,6 +786,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
     if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
     if (const char* e = getenv("ERGM_DW_SHIFT")) P->dw_shift = atoi(e) != 0;
+    if (const char* e = getenv("ERGM_FP8_MX")) P->mx = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -1002,6 +1037,10 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     uint8_t* qf = f8 && !P->dry ? P->qf + r0 * F : nullptr;
     float* sa = f8 && !P->dry ? P->sa + r0 : nullptr;
     float* sf = f8 && !P->dry ? P->sf + r0 : nullptr;
+    uint8_t* xa = f8 && !P->dry ? P->xa + r0 * (E / 32) : nullptr;  // MX block scales of qa / qf rows
+    uint8_t* xf = f8 && !P->dry ? P->xf + r0 * (F / 32) : nullptr;
+    float* lsa = P->mx ? nullptr : sa;  // the LayerNorms' fp8 copy: per-row scale or MX block scales
+    uint8_t* lxa = P->mx ? xa : nullptr;
     if (on(0) && w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
     // dropout sites of this block over the chain's rows (src/model.py:142 probabilities, :245 / :266
     // residual branches)
@@ -1011,11 +1050,11 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // self-attention sub-block (src/model.py:297-309)
     if (on(0) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
-                                  d.eps, s, qa, E, sa));
+                                  d.eps, s, qa, E, lsa, lxa, E / 32));
     if (on(1)) {
         if (f8)
-            ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr, a.qkv, 3 * E,
-                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
+            ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, xa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr,
+                           w8 ? w8->sx[0] : nullptr, a.qkv, 3 * E, ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
         else
             ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
@@ -1025,9 +1064,10 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
                                &dp_self, attn_bits(P, l, 0, b0), s));
     if (on(3)) {
         if (f8) {
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.ao, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr, x1, E, ERGM_F32,
-                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, &dr_attn));
+            if (!P->dry) ERGM_TRY(quant_act(P, a.ao, P->XE, T, E, qa, sa, xa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr,
+                           w8 ? w8->sx[1] : nullptr, x1, E, ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E,
+                           nullptr, 0, &dr_attn));
         } else {
             ERGM_TRY(gemm(P, s, T, E, E, a.ao, P->XE, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_KN, x1, E, ERGM_F32,
                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E, nullptr, 0, nullptr, &dr_attn));
@@ -1036,11 +1076,11 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // cross-attention over caption embeddings (src/model.py:311-329)
     if (on(4) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
-                                  d.eps, s, qa, E, sa));
+                                  d.eps, s, qa, E, lsa, lxa, E / 32));
     if (on(5)) {
         if (f8)
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr, a.xq, E, ERGM_BF16,
-                           ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr,
+                           w8 ? w8->sx[2] : nullptr, a.xq, E, ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
         else
             ERGM_TRY(gemm(P, s, T, E, E, a.lnx, P->XE, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_KN, a.xq, E, ERGM_BF16,
                           ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
@@ -1052,9 +1092,10 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
                                attn_bits(P, l, 1, b0), s));
     if (on(7)) {
         if (f8) {
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.xo, ERGM_BF16, P->XE, T, E, qa, E, sa, s));
-            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr, x2, E, ERGM_F32,
-                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, &dr_cross));
+            if (!P->dry) ERGM_TRY(quant_act(P, a.xo, P->XE, T, E, qa, sa, xa, s));
+            ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr,
+                           w8 ? w8->sx[3] : nullptr, x2, E, ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E,
+                           nullptr, 0, &dr_cross));
         } else {
             ERGM_TRY(gemm(P, s, T, E, E, a.xo, P->XE, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_KN, x2, E, ERGM_F32,
                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E, nullptr, 0, nullptr, &dr_cross));
@@ -1063,16 +1104,19 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // MLP (src/model.py:331-334, 262-267)
     if (on(8) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
-                                  d.eps, s, qa, E, sa));
+                                  d.eps, s, qa, E, lsa, lxa, E / 32));
     if (f8) {
         if (on(9)) {
-            ERGM_TRY(gemm8(P, s, T, F, E, qa, sa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr, a.act, P->XF,
-                           ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B), nullptr, 0, a.pre, F));
-            if (!P->dry) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
+            // MX: the GELU epilogue writes the MX copy of its output itself (no quantisation pass)
+            ERGM_TRY(gemm8(P, s, T, F, E, qa, sa, xa, w8 ? w8->w[4] : nullptr, w8 ? w8->sc[4] : nullptr,
+                           w8 ? w8->sx[4] : nullptr, a.act, P->XF, ERGM_BF16, ERGM_EPI_BIAS_GELU, LF(P, l, ERGM_T_FC_B),
+                           nullptr, 0, a.pre, F, nullptr, P->mx ? qf : nullptr, P->mx ? xf : nullptr));
+            if (!P->dry && !P->mx) ERGM_TRY(quant_rows_fp8(a.act, ERGM_BF16, P->XF, T, F, qf, F, sf, s));
         }
         if (on(10))
-            ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr, x3, E, ERGM_F32,
-                           ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E, nullptr, 0, &dr_mlp));
+            ERGM_TRY(gemm8(P, s, T, E, F, qf, sf, xf, w8 ? w8->w[5] : nullptr, w8 ? w8->sc[5] : nullptr,
+                           w8 ? w8->sx[5] : nullptr, x3, E, ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_MPROJ_B), x2, E,
+                           nullptr, 0, &dr_mlp));
     } else {
         if (on(9))
             ERGM_TRY(gemm(P, s, T, F, E, a.ln2, P->XE, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_KN, a.act, P->XF,
@@ -1165,18 +1209,26 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         if (train && !P->dry)
             ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
         if (P->f8 && !P->dry) {
-            if (hipMemsetAsync(P->capkv_amax, 0, (size_t)L2E * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "memset");
-            WqJobs J{};
-            J.n = 1;
-            J.j[0] = WqJob{p.capkv_w_b, P->capkv8, P->capkv8_s, P->capkv_amax, L2E, E, L2E, E, 0, 0, 1};
-            ERGM_TRY(quant_weights_fp8(J, ss));
-            ERGM_TRY(quant_rows_fp8(P->cap, ERGM_BF16, P->XE, T, E, P->qcap, E, P->scap, ss));
+            if (P->mx) {
+                MxJobs J{};
+                J.n = 1;
+                J.j[0] = MxJob{reinterpret_cast<const __bf16*>(p.capkv_w_b), P->capkv8, P->capkv8_x, L2E, E, L2E, E,
+                               E / 32, 0};
+                ERGM_TRY(quant_weights_mx(J, ss));
+            } else {
+                if (hipMemsetAsync(P->capkv_amax, 0, (size_t)L2E * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "memset");
+                WqJobs J{};
+                J.n = 1;
+                J.j[0] = WqJob{p.capkv_w_b, P->capkv8, P->capkv8_s, P->capkv_amax, L2E, E, L2E, E, 0, 0, 1};
+                ERGM_TRY(quant_weights_fp8(J, ss));
+            }
+            ERGM_TRY(quant_act(P, P->cap, P->XE, T, E, P->qcap, P->scap, P->xcap, ss));
         }
         {
             Probe pr(P, 4, ss);
             if (P->f8)
-                ERGM_TRY(gemm8(P, ss, T, L2E, E, P->qcap, P->scap, P->capkv8, P->capkv8_s, P->kv_all, L2E, ERGM_BF16,
-                               ERGM_EPI_BIAS, p.capkv_b));
+                ERGM_TRY(gemm8(P, ss, T, L2E, E, P->qcap, P->scap, P->xcap, P->capkv8, P->capkv8_s, P->capkv8_x,
+                               P->kv_all, L2E, ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b));
             else
                 ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E,
                               ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b));

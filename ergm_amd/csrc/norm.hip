@@ -17,7 +17,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ beta, __bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int E, int ldy, float eps, uint8_t* __restrict__ yq,
-                                                     int ldq, float* __restrict__ qscale) {
+                                                     int ldq, float* __restrict__ qscale, uint8_t* __restrict__ qmx,
+                                                     int ld_qmx) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;
@@ -66,7 +67,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
             amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
         }
     }
-    if (yq) {  // fp8 copy for the config-5 forward GEMMs (row scale, quant.hip's scheme)
+    if (yq && qmx) {  // MX-fp8 copy (config 5): a 32-column block is 8 consecutive lanes of one float4 group
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = (i * 64 + lane) * 4;
+            const bool in = c < E;  // E % 32 == 0: a block is wholly in or out
+            float am = in ? fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))) : 0.f;
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            am = fmaxf(am, __shfl_xor(am, 4, 64));
+            const int eb = mx_exp_biased(am);
+            const float is = mx_inv_scale(eb);
+            if (in) {
+                *reinterpret_cast<uint32_t*>(yq + (size_t)row * ldq + c) =
+                    mx_pack4(v[i].x * is, v[i].y * is, v[i].z * is, v[i].w * is);
+                if ((lane & 7) == 0) qmx[(size_t)row * ld_qmx + (c >> 5)] = (uint8_t)eb;
+            }
+        }
+    } else if (yq) {  // fp8 copy for the config-5 forward GEMMs (row scale, quant.hip's scheme)
         amax = wave_max(amax);
         const float sc = amax > 0.f ? amax / 448.f : 1.f;
 #pragma unroll
@@ -345,9 +363,11 @@ using namespace ergm;
 
 namespace ergm {
 int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void* y, int ldy, float* mean, float* rstd,
-                     int rows, int E, float eps, hipStream_t s, void* yq, int ldq, float* qscale) {
+                     int rows, int E, float eps, hipStream_t s, void* yq, int ldq, float* qscale, void* qmx, int ld_qmx) {
     if (diag_skip() & 16) return ERGM_OK;
-    ERGM_CHECK_ARG(!yq || (qscale && ldq >= E && ldq % 4 == 0), "layernorm_fwd: bad fp8 output");
+    ERGM_CHECK_ARG(!yq || ((qscale || qmx) && ldq >= E && ldq % 4 == 0), "layernorm_fwd: bad fp8 output");
+    ERGM_CHECK_ARG(!qmx || (E % 32 == 0 && ld_qmx >= E / 32), "layernorm_fwd: bad MX-fp8 output");
+    auto* qm = reinterpret_cast<uint8_t*>(qmx);
     auto* q8 = reinterpret_cast<uint8_t*>(yq);
     ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_fwd: unsupported E=%d", E);
@@ -356,10 +376,10 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
     int nv = cdiv(E, 256);
     auto* yb = reinterpret_cast<__bf16*>(y);
     switch (nv) {
-        case 1: ERGM_LAUNCH(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        case 2: ERGM_LAUNCH(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        case 3: ERGM_LAUNCH(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
-        default: ERGM_LAUNCH(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale); break;
+        case 1: ERGM_LAUNCH(ln_fwd_kernel<1>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale, qm, ld_qmx); break;
+        case 2: ERGM_LAUNCH(ln_fwd_kernel<2>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale, qm, ld_qmx); break;
+        case 3: ERGM_LAUNCH(ln_fwd_kernel<3>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale, qm, ld_qmx); break;
+        default: ERGM_LAUNCH(ln_fwd_kernel<4>, grid, dim3(256), 0, s, x, gamma, beta, yb, mean, rstd, rows, E, ldy, eps, q8, ldq, qscale, qm, ld_qmx); break;
     }
     return check_launch("layernorm_fwd");
 }
@@ -385,7 +405,8 @@ int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s) {
 
 extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, float* mean,
                                   float* rstd, int rows, int E, float eps, void* stream) {
-    return layernorm_fwd_ld(x, gamma, beta, y, E, mean, rstd, rows, E, eps, as_stream(stream), nullptr, 0, nullptr);
+    return layernorm_fwd_ld(x, gamma, beta, y, E, mean, rstd, rows, E, eps, as_stream(stream), nullptr, 0, nullptr,
+                            nullptr, 0);
 }
 
 extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {

@@ -216,6 +216,122 @@ int quant_weights_fp8(const WqJobs& J0, hipStream_t s) {
     return check_launch("quant_weights_fp8");
 }
 
+// ---- MX-fp8 (OCP microscaling; common.h mx_*): e8m0 scale per 32 consecutive elements along K ----------
+// Activations [rows][cols] -> Q [rows][ldq] e4m3 + S [rows][lds] e8m0 (block b = columns 32b..32b+31).  One row
+// per wavefront, 8 columns per lane per pass: a block is 4 consecutive lanes.
+template <bool BF16_IN>
+__global__ __launch_bounds__(256) void mx_quant_rows_kernel(const void* __restrict__ X, int ldx, int rows, int cols,
+                                                            uint8_t* __restrict__ Q, int ldq, uint8_t* __restrict__ S,
+                                                            int lds) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;
+    const size_t base = (size_t)row * ldx;
+    for (int c0 = 0; c0 < cols; c0 += 512) {  // cols % 32 == 0: a block is wholly in or out
+        const int c = c0 + lane * 8;
+        float v[8];
+        if (c < cols) load8(X, BF16_IN, base + c, v);
+        else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = 0.f;
+        }
+        uint2 q;
+        const int eb = mx_quant8_x4(v, q);
+        if (c < cols) {
+            *reinterpret_cast<uint2*>(Q + (size_t)row * ldq + c) = q;
+            if ((lane & 3) == 0) S[(size_t)row * lds + (c >> 5)] = (uint8_t)eb;
+        }
+    }
+}
+
+// Weights: MxJobs batched over one block's matrices.  Workgroup = (job, 64-row x 64-column tile of W); thread =
+// 4 consecutive rows x 4 consecutive columns; column maxima of each 32-row block merged through LDS, then the
+// quantised values packed per column (4 k-consecutive bytes) and written transposed through LDS as in
+// wq_quant_kernel, with the block scales.
+__device__ __forceinline__ int find_mx_job(const MxJobs& J, int bid) {
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+        if (i < J.n && bid >= J.j[i].blk) k = i;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void mx_quant_weight_kernel(MxJobs J) {
+    constexpr int LD = 80;
+    __shared__ __attribute__((aligned(16))) uint8_t tile[64 * LD];
+    __shared__ float red[16][64];
+    __shared__ int ebs[2][64];
+    const int ji = find_mx_job(J, blockIdx.x);
+    const MxJob& jb = J.j[ji];
+    const int local = blockIdx.x - jb.blk;
+    const int nt = jb.N / 64, kt = local / nt, n0 = (local % nt) * 64, k0 = kt * 64;
+    const int nq = (threadIdx.x & 15) * 4, kg = threadIdx.x >> 4, kq = kg * 4;
+    float w[4][4];  // [row][column]
+    float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bf16x4 x = *reinterpret_cast<const bf16x4*>(jb.W + (size_t)(k0 + kq + r) * jb.ldw + n0 + nq);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            w[r][j] = bf2f(x[j]);
+            cm[j] = fmaxf(cm[j], fabsf(w[r][j]));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[kg][nq + j] = cm[j];
+    __syncthreads();
+    if (threadIdx.x < 128) {  // (block h, column n): max over the 8 row groups of the block
+        const int h = threadIdx.x >> 6, n = threadIdx.x & 63;
+        float m = red[8 * h][n];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m = fmaxf(m, red[8 * h + i][n]);
+        const int eb = mx_exp_biased(m);
+        ebs[h][n] = eb;
+        jb.sc[(size_t)(n0 + n) * jb.lds + (k0 >> 5) + h] = (uint8_t)eb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float is = mx_inv_scale(ebs[kg >> 3][nq + j]);
+        *reinterpret_cast<uint32_t*>(tile + (nq + j) * LD + kq) =
+            mx_pack4(w[0][j] * is, w[1][j] * is, w[2][j] * is, w[3][j] * is);
+    }
+    __syncthreads();
+    const int n = threadIdx.x >> 2, q = threadIdx.x & 3;
+    *reinterpret_cast<uint4*>(jb.Wt + (size_t)(n0 + n) * jb.ldt + k0 + q * 16) =
+        *reinterpret_cast<const uint4*>(tile + n * LD + q * 16);
+}
+
+int quant_weights_mx(const MxJobs& J0, hipStream_t s) {
+    MxJobs J = J0;
+    ERGM_CHECK_ARG(J.n >= 1 && J.n <= 8, "quant_weights_mx: 1..8 matrices per launch");
+    int b = 0;
+    for (int i = 0; i < J.n; ++i) {
+        MxJob& j = J.j[i];
+        ERGM_CHECK_ARG(j.W && j.Wt && j.sc && j.N % 64 == 0 && j.K % 64 == 0 && j.ldt >= j.K && j.ldt % 16 == 0 &&
+                           j.ldw >= j.N && j.ldw % 4 == 0 && j.lds >= j.K / 32,
+                       "quant_weights_mx: bad matrix %d (K=%d N=%d)", i, j.K, j.N);
+        j.blk = b;
+        b += (j.N / 64) * (j.K / 64);
+    }
+    ERGM_LAUNCH(mx_quant_weight_kernel, dim3(b), dim3(256), 0, s, J);
+    return check_launch("quant_weights_mx");
+}
+
+int quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
+                  hipStream_t s) {
+    ERGM_CHECK_ARG(X && Q && S && rows > 0 && cols > 0 && cols % 32 == 0 && ldx % 8 == 0 && ldx >= cols &&
+                       ldq >= cols && ldq % 8 == 0 && lds >= cols / 32,
+                   "quant_rows_mx: bad argument");
+    ERGM_CHECK_ARG(x_dtype == ERGM_BF16 || x_dtype == ERGM_F32, "quant_rows_mx: bad dtype");
+    dim3 grid(cdiv(rows, 4));
+    auto* q = reinterpret_cast<uint8_t*>(Q);
+    auto* sc = reinterpret_cast<uint8_t*>(S);
+    if (x_dtype == ERGM_BF16) ERGM_LAUNCH(mx_quant_rows_kernel<true>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, sc, lds);
+    else ERGM_LAUNCH(mx_quant_rows_kernel<false>, grid, dim3(256), 0, s, X, ldx, rows, cols, q, ldq, sc, lds);
+    return check_launch("quant_rows_mx");
+}
+
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
                    hipStream_t s) {
     ERGM_CHECK_ARG(X && Q && scale && rows > 0 && cols > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldx >= cols &&
@@ -256,4 +372,18 @@ extern "C" int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K,
     J.j[0] = WqJob{W, reinterpret_cast<uint8_t*>(Wt), scale, reinterpret_cast<unsigned*>(amax_ws), ldw, K, N, ldt, 0, 0,
                    w_dtype == ERGM_BF16};
     return quant_weights_fp8(J, s);
+}
+
+extern "C" int ergm_quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S,
+                                  int lds, void* stream) {
+    return quant_rows_mx(X, x_dtype, ldx, rows, cols, Q, ldq, S, lds, as_stream(stream));
+}
+
+extern "C" int ergm_quant_weight_mx(const void* W, int ldw, int K, int N, void* Wt, int ldt, void* S, int lds,
+                                    void* stream) {
+    MxJobs J{};
+    J.n = 1;
+    J.j[0] = MxJob{reinterpret_cast<const __bf16*>(W), reinterpret_cast<uint8_t*>(Wt), reinterpret_cast<uint8_t*>(S), ldw,
+                   K, N, ldt, lds, 0};
+    return quant_weights_mx(J, as_stream(stream));
 }

@@ -97,6 +97,53 @@ def quant_weight_fp8(W: torch.Tensor):
     return Wt, sc
 
 
+def gemm_mx(A8: torch.Tensor, a_sc: torch.Tensor, B8t: torch.Tensor, b_sc: torch.Tensor,
+            out: Optional[torch.Tensor] = None, out_dtype=torch.float32, epilogue: int = L.EPI_NONE,
+            bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+            aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0, q_out: Optional[torch.Tensor] = None,
+            q_sc: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """MX-fp8 GEMM: C[M,N] = epilogue(alpha · Σ_k dequant(A8)[m,k]·dequant(B8t)[n,k]) with A8 [M,K], B8t [N,K]
+    e4m3 bytes and their e8m0 block scales a_sc [M,K/32], b_sc [N,K/32] (uint8, 2^(byte-127) per 32-element K
+    block).  q_out / q_sc (BIAS_GELU): the MX copy of the bf16 output ([M,N] / [M,N/32] uint8)."""
+    _need_gpu(A8, B8t, a_sc, b_sc)
+    M, K = A8.shape
+    N = B8t.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=A8.device)
+    d = L.GemmDesc(M=M, N=N, K=K, lda=A8.stride(0), ldb=B8t.stride(0), ldc=out.stride(0), a_layout=L.MK,
+                   b_layout=L.NK, c_dtype=L.BF16 if out.dtype == torch.bfloat16 else L.F32, epilogue=epilogue,
+                   alpha=alpha, bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
+                   aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0)
+    L.check(L.load().ergm_gemm_mx(C.byref(d), _ptr(A8), _ptr(a_sc), a_sc.stride(0), _ptr(B8t), _ptr(b_sc),
+                                  b_sc.stride(0), _ptr(out), _ptr(q_out), _ptr(q_sc),
+                                  q_out.stride(0) if q_out is not None else 0,
+                                  q_sc.stride(0) if q_sc is not None else 0, _stream(A8.device)), "ergm_gemm_mx")
+    return out
+
+
+def quant_rows_mx(X: torch.Tensor, cols: Optional[int] = None):
+    """MX-fp8 quantisation of rows: returns (Q [rows, cols] uint8 e4m3, S [rows, cols/32] uint8 e8m0)."""
+    _need_gpu(X)
+    rows = X.shape[0]
+    cols = X.shape[1] if cols is None else cols
+    Q = torch.empty(rows, cols, dtype=torch.uint8, device=X.device)
+    S = torch.empty(rows, cols // 32, dtype=torch.uint8, device=X.device)
+    dt = L.BF16 if X.dtype == torch.bfloat16 else L.F32
+    L.call("ergm_quant_rows_mx", _ptr(X), dt, X.stride(0), rows, cols, _ptr(Q), cols, _ptr(S), cols // 32,
+           _stream(X.device))
+    return Q, S
+
+
+def quant_weight_mx(W: torch.Tensor):
+    """Conv1D weight W [K, N] (bf16) → (Wt [N, K] e4m3 bytes, S [N, K/32] e8m0 block scales)."""
+    _need_gpu(W)
+    K, N = W.shape
+    Wt = torch.empty(N, K, dtype=torch.uint8, device=W.device)
+    S = torch.empty(N, K // 32, dtype=torch.uint8, device=W.device)
+    L.call("ergm_quant_weight_mx", _ptr(W), W.stride(0), K, N, _ptr(Wt), K, _ptr(S), K // 32, _stream(W.device))
+    return Wt, S
+
+
 def dropout_desc(p: float, seed: int, offset: int, site: int, row0: int = 0) -> L.Dropout:
     """ergm_dropout for one site of one forward (include/ergm_hip.h)."""
     return L.Dropout(seed=seed & (2 ** 64 - 1), offset=offset & 0xFFFFFFFF, site=site, p=p, row0=row0)
