@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 6  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 7  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -83,7 +83,7 @@ _SIGS = {
     "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp]),
     "ergm_gemm_mx": (i32, [C.POINTER(GemmDesc), vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]),
     "ergm_quant_rows_mx": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, i32, vp]),
-    "ergm_quant_weight_mx": (i32, [vp, i32, i32, i32, vp, i32, vp, i32, vp]),
+    "ergm_quant_weight_mx": (i32, [vp, i32, i32, i32, vp, i32, vp, i32, vp, i32, vp, i32, vp]),
     "ergm_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "ergm_attn_tune": (i32, [i32]),
     "ergm_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp] + [i32] * 13 + [vp, vp, vp]),

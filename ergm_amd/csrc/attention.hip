@@ -96,6 +96,10 @@ struct AttnArgs {
     DropSite drop;
     uint64_t* mbits;
     int mwords;  // u64 words per row = ceil(Sk / 64)
+    // MX-fp8 copy of the forward output (config 5): e4m3 [row][ldqm] and e8m0 scales in common.h's mx_sidx
+    // layout (pitch qpitch rows), row = b·Sq + q; nullptr: none
+    uint8_t *qmx, *qms;
+    int ldqm, qpitch;
 };
 
 // Dropout factor of one probability: 1/(1-p) kept, 0 dropped.
@@ -232,8 +236,35 @@ __device__ __forceinline__ float stored_keep(const uint64_t* mrow, int key, floa
 __device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q, const f32x4 (&o)[4], float m,
                                           float l) {
     const int g = (threadIdx.x & 63) >> 4;
-    if (q >= a.Sq) return;
     const float inv = l > 0.f ? 1.0f / l : 0.f;
+    if (a.qmx) {  // MX copy of the stored bf16 row: block 0 = dims 0-31 (d = 0, 1), block 1 = 32-63, each spread over
+                  // the 4 lanes of this query (l, l^16, l^32, l^48); all lanes take part in the row reductions
+        const bool live = q < a.Sq;
+        const size_t row = (size_t)b * a.Sq + q;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            float v[2][4];
+            float am = 0.f;
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[dd][r] = live ? bf2f(f2bf(o[2 * half + dd][r] * inv)) : 0.f;
+                    am = fmaxf(am, fabsf(v[dd][r]));
+                }
+            am = rows_max(am);
+            const int eb = mx_exp_biased(am);
+            const float is = mx_inv_scale(eb);
+            if (live) {
+#pragma unroll
+                for (int dd = 0; dd < 2; ++dd)
+                    *reinterpret_cast<uint32_t*>(a.qmx + row * a.ldqm + h * AT_D + (2 * half + dd) * 16 + 4 * g) =
+                        mx_pack4(v[dd][0] * is, v[dd][1] * is, v[dd][2] * is, v[dd][3] * is);
+                if (g == 0) a.qms[mx_sidx((int)row, 2 * h + half, a.qpitch)] = (uint8_t)eb;
+            }
+        }
+    }
+    if (q >= a.Sq) return;
     __bf16* Ob = a.out + ((size_t)b * a.Sq + q) * a.ldo + h * AT_D;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -882,9 +913,23 @@ extern "C" int ergm_attn_tune(int force_generic) {
     return ERGM_OK;
 }
 
+namespace ergm {
+// ergm_attn_fwd + the MX-fp8 copy of its output (the executor's config-5 forward: the c_proj GEMMs' A operand)
+int attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk, int ldq,
+                int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits, uint8_t* qmx,
+                uint8_t* qms, int ldqm, int qpitch, hipStream_t s);
+}
+
 extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout,
                              void* keep_bits, void* stream) {
+    return ergm::attn_fwd_mx(q, k, v, o, lse, B, H, Sq, Sk, ldq, ldk, ldv, ldo, causal, dropout, keep_bits, nullptr,
+                             nullptr, 0, 0, as_stream(stream));
+}
+
+int ergm::attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
+                      int ldq, int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits,
+                      uint8_t* qmx, uint8_t* qms, int ldqm, int qpitch, hipStream_t s) {
     if (diag_skip() & 64) return ERGM_OK;
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && lse && ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd: bad output");
@@ -895,7 +940,8 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
     a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
     a.scale = 0.125f;  // 1/sqrt(64): exact, so x*scale == x / 8.0 (src/model.py:122-125)
     ERGM_TRY(set_drop(a, dropout, keep_bits));
-    hipStream_t s = as_stream(stream);
+    ERGM_CHECK_ARG(!qmx || (qms && ldqm >= H * AT_D && ldqm % 4 == 0 && qpitch >= B * Sq), "attn_fwd: bad MX output");
+    a.qmx = qmx; a.qms = qms; a.ldqm = ldqm; a.qpitch = qpitch;
     // every length takes the tiled kernel: at S = 128 its 2x more workgroups beat the one-workgroup-per-
     // (b, h) form inside the concurrent step (C2 +1.6 %, C5 +0.4 %; profiles/r01_overlap_experiments.txt #19)
     dim3 grid(cdiv(Sq, AT_T), H, B);

@@ -108,13 +108,17 @@ struct WqJobs {
     int n;
 };
 // MX-fp8 weight quantisation jobs (quant.hip): W [K][ldw] bf16 -> Wt [N][ldt] e4m3 (transposed) with an e8m0
-// scale per (column, 32-row block): sc [N][lds]
+// scale per (column, 32-row block): sc [N][lds]; optionally also the row form Wr [K][ldr] e4m3 with a scale per
+// (row, 32-column block): scr [K][ldsr] (the B operand of the data-gradient GEMM dX = dY·Wᵀ)
 struct MxJob {
     const __bf16* W;
     uint8_t* Wt;
     uint8_t* sc;
     int ldw, K, N, ldt, lds;
     int blk;  // first block of this job in the grid (set by quant_weights_mx)
+    uint8_t* Wr;
+    uint8_t* scr;
+    int ldr, ldsr;
 };
 struct MxJobs {
     MxJob j[8];
@@ -211,6 +215,13 @@ __device__ __forceinline__ bool drop_keep1(const DropSite& d, int64_t row, int c
 // Block exponent: the smallest e with amax <= 448·2^e (no element saturates), from the bits of amax: amax =
 // 1.f·2^ea gives e = ea - 8, or ea - 7 when 1.f > 1.75 (448 = 1.75·2^8).  A zero block gets e = 0 (scale 1).
 // Returned biased (e + 127, clamped to [0, 254]); the scaled values v·2^-e are exact in f32.
+// MX scale layout: the e8m0 bytes of a 128-deep K step (4 blocks) of every row are one 4-byte word, and the words of
+// one K step are contiguous over the rows: byte (row, block b) at ((b / 4) * pitch + row) * 4 + b % 4, pitch >= the
+// row count.  A GEMM stage's scale loads are then whole cache lines (64 rows = 256 contiguous bytes) instead of one
+// 4-byte piece of 64 different rows.
+__device__ __forceinline__ size_t mx_sidx(int row, int blk, int pitch) {
+    return ((size_t)(blk >> 2) * pitch + row) * 4 + (blk & 3);
+}
 __device__ __forceinline__ int mx_exp_biased(float amax) {
     const uint32_t b = __float_as_uint(amax);
     if (amax == 0.f) return 127;

@@ -195,7 +195,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
                 const int eb = mx_quant8_x4(v, q);
                 if (ok) {
                     *reinterpret_cast<uint2*>(a.q_out + (size_t)m * a.ld_q + n) = q;
-                    if ((c & 3) == 0) a.q_sc[(size_t)m * a.ld_qs + (n >> 5)] = (uint8_t)eb;
+                    if ((c & 3) == 0) a.q_sc[mx_sidx(m, n >> 5, a.ld_qs)] = (uint8_t)eb;
                 }
                 continue;
             }
@@ -822,10 +822,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmArgs a) {
 }
 
 // MX-fp8 GEMM (OCP microscaling, config 5's forward): A [M][K] and B [N][K] e4m3 bytes (k contiguous) with an
-// e8m0 scale per 32-element K block of every row of A (a_mx [M][ld_sa]) and of B (b_mx [N][ld_sb]), consumed
-// by the MFMA itself: v_mfma_scale_f32_16x16x128_f8f6f4 takes the 32 bytes a lane holds (row l&15, K block
-// l>>4 of the 128-deep step) with that lane's scale byte.  The scales of a stage (4 bytes per row: the 4
-// blocks of a 128-deep step) ride in the same LDS ring behind the operand tiles, filled by 4-byte-per-lane
+// e8m0 scale per 32-element K block of every row of A (a_mx, pitch ld_sa rows) and of B (b_mx, pitch ld_sb rows) in
+// the K-step-major layout of common.h mx_sidx, consumed by the MFMA itself: v_mfma_scale_f32_16x16x128_f8f6f4
+// applies lane group G's scale byte to K [32G, 32G+32) of the 128-deep step (frag_mx).  The scales of a stage
+// (4 bytes per row: the 4 blocks of a 128-deep step, 256 contiguous bytes per 64 rows) ride in the same LDS ring
+// behind the operand tiles, filled by 4-byte-per-lane
 // LDS-DMA (one 64-row piece per wave-instruction; with more waves than pieces the spare waves re-issue piece
 // 0, identical bytes, so every wave issues the same count and the counted waits stay exact).  No
 // per-row / per-column dequantisation in the epilogue; QMX: the epilogue also writes an MX copy of its bf16
@@ -875,8 +876,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_mx_kernel(GemmArgs a) {
             if (p >= NSP) p = 0;  // spare wave: re-issue piece 0 (same bytes, same destination)
             const bool isb = p * 64 >= BM;
             const int r = (isb ? p * 64 - BM : p * 64) + lane;
-            const uint8_t* src = isb ? a.b_mx + (size_t)min(n0 + r, a.N - 1) * a.ld_sb + kt * 4
-                                     : a.a_mx + (size_t)min(m0 + r, a.M - 1) * a.ld_sa + kt * 4;
+            const uint8_t* src = isb ? a.b_mx + ((size_t)kt * a.ld_sb + min(n0 + r, a.N - 1)) * 4
+                                     : a.a_mx + ((size_t)kt * a.ld_sa + min(m0 + r, a.M - 1)) * 4;
             glds4(src, __builtin_amdgcn_readfirstlane(lds_addr_of(st + A_BYTES + B_BYTES + p * 256)));
         }
     };
@@ -1382,24 +1383,23 @@ extern "C" int ergm_gemm_mx(const ergm_gemm_desc* d, const void* A, const void* 
     ERGM_CHECK_ARG(d->a_layout == ERGM_MK && d->b_layout == ERGM_NK, "ergm_gemm_mx: A [M][K] and B [N][K] only");
     ERGM_CHECK_ARG(d->lda >= d->K && d->ldb >= d->K && d->lda % 16 == 0 && d->ldb % 16 == 0,
                    "ergm_gemm_mx: lda/ldb >= K, multiples of 16 bytes");
-    ERGM_CHECK_ARG(ld_sa >= d->K / 32 && ld_sb >= d->K / 32 && ld_sa % 4 == 0 && ld_sb % 4 == 0,
-                   "ergm_gemm_mx: scale rows >= K/32 bytes, multiples of 4");
+    ERGM_CHECK_ARG(ld_sa >= d->M && ld_sb >= d->N, "ergm_gemm_mx: scale pitches ld_sa >= M, ld_sb >= N (rows)");
     ERGM_CHECK_ARG(aligned16(A) && aligned16(B) && (reinterpret_cast<uintptr_t>(a_scale) & 3) == 0 &&
                        (reinterpret_cast<uintptr_t>(b_scale) & 3) == 0,
                    "ergm_gemm_mx: operand / scale alignment");
     ERGM_CHECK_ARG(d->N % 8 == 0 && d->ldc % 8 == 0 && d->ldc >= d->N, "ergm_gemm_mx: N, ldc multiples of 8");
     ERGM_CHECK_ARG(d->c_dtype == ERGM_F32 || d->c_dtype == ERGM_BF16, "ergm_gemm_mx: bad c_dtype");
     const int e = d->epilogue;
-    ERGM_CHECK_ARG((e == ERGM_EPI_NONE || e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) ? d->c_dtype == ERGM_BF16 ||
-                       e == ERGM_EPI_NONE
-                                                                                        : e == ERGM_EPI_BIAS_RESID &&
-                                                                                              d->c_dtype == ERGM_F32,
+    const bool bf_epi = e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU || e == ERGM_EPI_GELU_BWD;
+    ERGM_CHECK_ARG(e == ERGM_EPI_NONE || (bf_epi && d->c_dtype == ERGM_BF16) ||
+                       (e == ERGM_EPI_BIAS_RESID && d->c_dtype == ERGM_F32),
                    "ergm_gemm_mx: epilogue %d with c_dtype %d not supported", e, d->c_dtype);
-    ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_RESID || (d->aux && d->ld_aux % 8 == 0), "ergm_gemm_mx: residual needs aux");
+    ERGM_CHECK_ARG(!(e == ERGM_EPI_BIAS_RESID || e == ERGM_EPI_GELU_BWD) || (d->aux && d->ld_aux % 8 == 0),
+                   "ergm_gemm_mx: epilogue %d needs aux", e);
     ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || (d->aux_out && d->ld_aux_out % 8 == 0), "ergm_gemm_mx: GELU needs aux_out");
-    ERGM_CHECK_ARG(!q_out || (q_scale && e == ERGM_EPI_BIAS_GELU && d->N % 32 == 0 && ld_q >= d->N && ld_q % 8 == 0 &&
-                              ld_qs >= d->N / 32),
-                   "ergm_gemm_mx: the MX copy of C needs the BIAS_GELU epilogue, N % 32 == 0 and its buffers");
+    ERGM_CHECK_ARG(!q_out || (q_scale && (e == ERGM_EPI_BIAS_GELU || e == ERGM_EPI_GELU_BWD) && d->N % 32 == 0 &&
+                              ld_q >= d->N && ld_q % 8 == 0 && ld_qs >= d->M),
+                   "ergm_gemm_mx: the MX copy of C needs a GELU / GELU' epilogue, N % 32 == 0 and its buffers");
     const int cfg = plan_f8(d->M, d->N);
     GemmArgs a;
     memset(&a, 0, sizeof(a));
@@ -1435,6 +1435,10 @@ extern "C" int ergm_gemm_mx(const ergm_gemm_desc* d, const void* A, const void* 
         case ERGM_EPI_BIAS_GELU:
             if (q_out) launch_mx<ERGM_EPI_BIAS_GELU, true, true>(a, cfg, s);
             else launch_mx<ERGM_EPI_BIAS_GELU, true, false>(a, cfg, s);
+            break;
+        case ERGM_EPI_GELU_BWD:
+            if (q_out) launch_mx<ERGM_EPI_GELU_BWD, true, true>(a, cfg, s);
+            else launch_mx<ERGM_EPI_GELU_BWD, true, false>(a, cfg, s);
             break;
         default: launch_mx<ERGM_EPI_BIAS_RESID, false, false>(a, cfg, s); break;
     }

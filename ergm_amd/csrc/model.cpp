@@ -30,6 +30,9 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
                      void* qmx = nullptr, int ld_qmx = 0);
 int quant_weights_fp8(const WqJobs& J, hipStream_t s);
 int quant_weights_mx(const MxJobs& J, hipStream_t s);
+int attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk, int ldq,
+                int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits, uint8_t* qmx,
+                uint8_t* qms, int ldqm, int qpitch, hipStream_t s);
 int quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
                   hipStream_t s);
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
@@ -38,7 +41,7 @@ int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop, int drop_res);
+                       const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs);
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
@@ -74,6 +77,8 @@ struct LayerW8 {
     uint8_t* w[6];
     float* sc[6];
     uint8_t* sx[6];  // MX-fp8: e8m0 scale per (column, 32-row block), [N][K/32]
+    uint8_t* wr[6];  // MX-fp8 row form (fp8 data-gradient GEMMs): W [K][N] e4m3, scale per (row, 32-column block)
+    uint8_t* sr[6];  // [K][N/32]
     unsigned* amax;
     int amax_n;
 };
@@ -124,6 +129,12 @@ struct ergm_model_plan {
     // every activation row and weight column, consumed by the MFMA (ergm_gemm_mx); the LayerNorms and the c_fc
     // GELU epilogue write their MX copies themselves, the weights are quantised in one pass (no amax pass)
     bool mx = true;
+    // fp8 data-gradient GEMMs (config 5 with MX, ERGM_FP8_BWD): dX = dY·Wᵀ on MX operands — the LayerNorm backward
+    // writes the MX copy of the residual-branch gradient it stores (dhq / dhx), the mlp c_proj dX epilogue that of
+    // the GELU' output (dpq / dpx), the attention-backward outputs take a row pass (gq / gx); the weights' row form
+    // is quantised with their transposed forward copy.  The weight gradients stay bf16.
+    bool mxb = false;
+    uint8_t *dhq, *dhx, *dpq, *dpx, *gq, *gx;
     std::vector<LayerW8> w8;
     uint8_t *capkv8, *qa, *qf, *qcap;
     float *capkv8_s, *sa, *sf, *scap;
@@ -286,6 +297,7 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->capkv8 = P->qa = P->qf = P->qcap = nullptr;
     P->capkv8_s = P->sa = P->sf = P->scap = nullptr;
     P->capkv8_x = P->xa = P->xf = P->xcap = nullptr;
+    P->dhq = P->dhx = P->dpq = P->dpx = P->gq = P->gx = nullptr;
     P->capkv_amax = nullptr;
     if (P->f8) {
         const size_t KN[6][2] = {{E, 3 * E}, {E, E}, {E, E}, {E, E}, {E, F}, {F, E}};
@@ -296,6 +308,8 @@ size_t carve(ergm_model_plan* P, char* base) {
                 w.w[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
                 w.sc[i] = c.take<float>(KN[i][1]);
                 w.sx[i] = c.take<uint8_t>(KN[i][0] / 32 * KN[i][1]);
+                w.wr[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
+                w.sr[i] = c.take<uint8_t>(KN[i][0] * (KN[i][1] / 32));
                 na += (int)KN[i][1];
             }
             w.amax = c.take<unsigned>(na);
@@ -314,6 +328,12 @@ size_t carve(ergm_model_plan* P, char* base) {
         P->xa = c.take<uint8_t>(T * (E / 32));
         P->xf = c.take<uint8_t>(T * (F / 32));
         P->xcap = c.take<uint8_t>(T * (E / 32));
+        P->dhq = c.take<uint8_t>(T * E);
+        P->dhx = c.take<uint8_t>(T * (E / 32));
+        P->dpq = c.take<uint8_t>(T * F);
+        P->dpx = c.take<uint8_t>(T * (F / 32));
+        P->gq = c.take<uint8_t>(T * 3 * E);
+        P->gx = c.take<uint8_t>(T * (3 * E / 32));
     }
     P->Fd = d.feat_dim > 0 ? d.feat_dim : (int)E;
     P->proj = d.has_features && P->Fd != (int)E;
@@ -435,20 +455,23 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
           const void* aux = nullptr, int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0,
           const ergm_dropout* dropout = nullptr, uint8_t* qo = nullptr, uint8_t* qox = nullptr) {
     if (P->dry) return ERGM_OK;
+    if (diag_skip() & P->diag_cls) return ERGM_OK;
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
     g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = ldc;
     g.a_layout = ERGM_MK; g.b_layout = ERGM_NK; g.c_dtype = cdt; g.epilogue = epi; g.alpha = 1.0f;
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
     g.dropout = dropout;
-    if (P->mx) return ergm_gemm_mx(&g, A, ax, K / 32, Bt, bx, K / 32, C, qo, qox, N, N / 32, s);
+    // MX scale pitches (mx_sidx): activation rows (A, the MX copy of C) are token rows of a T-row buffer, B is a
+    // weight copy with exactly N rows
+    if (P->mx) return ergm_gemm_mx(&g, A, ax, P->T, Bt, bx, N, C, qo, qox, N, P->T, s);
     return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
 }
 // Row quantisation of an fp8 GEMM's activation operand (attention outputs, caption embeddings; the GELU output
 // too without MX): per-row scale `sf` or MX block scales `sx`.
 int quant_act(ergm_model_plan* P, const void* X, int ldx, int rows, int cols, uint8_t* q, float* sf, uint8_t* sx,
               hipStream_t s) {
-    if (P->mx) return quant_rows_mx(X, ERGM_BF16, ldx, rows, cols, q, cols, sx, cols / 32, s);
+    if (P->mx) return quant_rows_mx(X, ERGM_BF16, ldx, rows, cols, q, cols, sx, P->T, s);
     return quant_rows_fp8(X, ERGM_BF16, ldx, rows, cols, q, cols, sf, s);
 }
 
@@ -631,8 +654,10 @@ int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* 
     // itself goes through the embedding dropout (src/model.py:506), folded into this pass.
     const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
     const int fin = slot == 0;
+    const bool q = !fin && P->f8 && P->mx && P->mxb;  // the MX copy for the fp8 data-gradient GEMM that reads dh_b
     return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
-                              pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin);
+                              pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin, q ? P->dhq + o : nullptr,
+                              q ? P->dhx + (size_t)r0 * 4 : nullptr, T);
 }
 int ln_reduce_add(ergm_model_plan* P, int slot, float* dgamma, float* dbeta) {
     if (P->dry) return ERGM_OK;
@@ -684,7 +709,15 @@ int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
     if (P->mx) {  // one pass: block scales from each 32-row block's own maxima
         MxJobs J{};
         J.n = 6;
-        for (int i = 0; i < 6; ++i) J.j[i] = MxJob{LB(P, l, tens[i]), w.w[i], w.sx[i], N[i], K[i], N[i], K[i], K[i] / 32, 0};
+        for (int i = 0; i < 6; ++i) {
+            J.j[i] = MxJob{LB(P, l, tens[i]), w.w[i], w.sx[i], N[i], K[i], N[i], K[i], N[i], 0};
+            if (P->mxb) {  // + the row form for the fp8 data-gradient GEMMs
+                J.j[i].Wr = w.wr[i];
+                J.j[i].scr = w.sr[i];
+                J.j[i].ldr = N[i];
+                J.j[i].ldsr = K[i];
+            }
+        }
         ERGM_TRY(quant_weights_mx(J, ss));
         return hipEventRecord(P->ev_wq[l], ss) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: event record");
     }
@@ -787,6 +820,11 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
     if (const char* e = getenv("ERGM_DW_SHIFT")) P->dw_shift = atoi(e) != 0;
     if (const char* e = getenv("ERGM_FP8_MX")) P->mx = atoi(e) != 0;
+    // fp8 data-gradient GEMMs: opt-in (ERGM_FP8_BWD=1).  Measured at C5 (tools/r3_mxb.sh): 1373-1381 utt/s vs
+    // 1419-1421 with the bf16 backward — the f32-output dX GEMMs run 2.2x faster in-step, but the GELU' dX, the
+    // row passes over the attention gradients and the weights' second (row-form) copy cost more than that
+    P->mxb = false;
+    if (const char* e = getenv("ERGM_FP8_BWD")) P->mxb = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -1037,8 +1075,8 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     uint8_t* qf = f8 && !P->dry ? P->qf + r0 * F : nullptr;
     float* sa = f8 && !P->dry ? P->sa + r0 : nullptr;
     float* sf = f8 && !P->dry ? P->sf + r0 : nullptr;
-    uint8_t* xa = f8 && !P->dry ? P->xa + r0 * (E / 32) : nullptr;  // MX block scales of qa / qf rows
-    uint8_t* xf = f8 && !P->dry ? P->xf + r0 * (F / 32) : nullptr;
+    uint8_t* xa = f8 && !P->dry ? P->xa + r0 * 4 : nullptr;  // MX block scales of qa / qf rows (pitch T, mx_sidx)
+    uint8_t* xf = f8 && !P->dry ? P->xf + r0 * 4 : nullptr;
     float* lsa = P->mx ? nullptr : sa;  // the LayerNorms' fp8 copy: per-row scale or MX block scales
     uint8_t* lxa = P->mx ? xa : nullptr;
     if (on(0) && w8 && hipStreamWaitEvent(s, P->ev_wq[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
@@ -1050,7 +1088,7 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // self-attention sub-block (src/model.py:297-309)
     if (on(0) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x0, LF(P, l, ERGM_T_LN1_W), LF(P, l, ERGM_T_LN1_B), a.ln1, P->XE, a.m1, a.r1, T, E,
-                                  d.eps, s, qa, E, lsa, lxa, E / 32));
+                                  d.eps, s, qa, E, lsa, lxa, P->T));
     if (on(1)) {
         if (f8)
             ERGM_TRY(gemm8(P, s, T, 3 * E, E, qa, sa, xa, w8 ? w8->w[0] : nullptr, w8 ? w8->sc[0] : nullptr,
@@ -1059,12 +1097,14 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
             ERGM_TRY(gemm(P, s, T, 3 * E, E, a.ln1, P->XE, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E, ERGM_KN, a.qkv, 3 * E,
                           ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_ATTN_B)));
     }
+    // MX: the attention kernels write the c_proj GEMMs' MX operand themselves
+    const bool amx = f8 && P->mx;
     if (on(2) && !P->dry)
-        ERGM_TRY(ergm_attn_fwd(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, nb, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
-                               &dp_self, attn_bits(P, l, 0, b0), s));
+        ERGM_TRY(attn_fwd_mx(a.qkv, a.qkv + E, a.qkv + 2 * E, a.ao, a.lse, nb, H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 1,
+                             &dp_self, attn_bits(P, l, 0, b0), amx ? qa : nullptr, amx ? xa : nullptr, E, P->T, s));
     if (on(3)) {
         if (f8) {
-            if (!P->dry) ERGM_TRY(quant_act(P, a.ao, P->XE, T, E, qa, sa, xa, s));
+            if (!P->dry && !amx) ERGM_TRY(quant_act(P, a.ao, P->XE, T, E, qa, sa, xa, s));
             ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[1] : nullptr, w8 ? w8->sc[1] : nullptr,
                            w8 ? w8->sx[1] : nullptr, x1, E, ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_APROJ_B), x0, E,
                            nullptr, 0, &dr_attn));
@@ -1076,7 +1116,7 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // cross-attention over caption embeddings (src/model.py:311-329)
     if (on(4) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
-                                  d.eps, s, qa, E, lsa, lxa, E / 32));
+                                  d.eps, s, qa, E, lsa, lxa, P->T));
     if (on(5)) {
         if (f8)
             ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr,
@@ -1088,11 +1128,11 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
     if (on(6) && l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
     if (on(6) && !P->dry)
-        ERGM_TRY(ergm_attn_fwd(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
-                               attn_bits(P, l, 1, b0), s));
+        ERGM_TRY(attn_fwd_mx(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
+                             attn_bits(P, l, 1, b0), amx ? qa : nullptr, amx ? xa : nullptr, E, P->T, s));
     if (on(7)) {
         if (f8) {
-            if (!P->dry) ERGM_TRY(quant_act(P, a.xo, P->XE, T, E, qa, sa, xa, s));
+            if (!P->dry && !amx) ERGM_TRY(quant_act(P, a.xo, P->XE, T, E, qa, sa, xa, s));
             ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[3] : nullptr, w8 ? w8->sc[3] : nullptr,
                            w8 ? w8->sx[3] : nullptr, x2, E, ERGM_F32, ERGM_EPI_BIAS_RESID, LF(P, l, ERGM_T_XPROJ_B), x1, E,
                            nullptr, 0, &dr_cross));
@@ -1104,7 +1144,7 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     // MLP (src/model.py:331-334, 262-267)
     if (on(8) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x2, LF(P, l, ERGM_T_LN2_W), LF(P, l, ERGM_T_LN2_B), a.ln2, P->XE, a.m2, a.r2, T, E,
-                                  d.eps, s, qa, E, lsa, lxa, E / 32));
+                                  d.eps, s, qa, E, lsa, lxa, P->T));
     if (f8) {
         if (on(9)) {
             // MX: the GELU epilogue writes the MX copy of its output itself (no quantisation pass)
@@ -1213,7 +1253,7 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                 MxJobs J{};
                 J.n = 1;
                 J.j[0] = MxJob{reinterpret_cast<const __bf16*>(p.capkv_w_b), P->capkv8, P->capkv8_x, L2E, E, L2E, E,
-                               E / 32, 0};
+                               L2E, 0};
                 ERGM_TRY(quant_weights_mx(J, ss));
             } else {
                 if (hipMemsetAsync(P->capkv_amax, 0, (size_t)L2E * 4, ss) != hipSuccess) return fail(ERGM_EHIP, "memset");
@@ -1394,6 +1434,12 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
     auto Tc = [&](int c) { return ch.nb[c] * S; };
     auto lnrow = [&](const float* p, int c) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S; };
+    // fp8 data-gradient GEMMs (P->mxb): MX operands of dY (chain rows) and of the weights' row form
+    const bool xb = P->f8 && P->mx && P->mxb;
+    const LayerW8* w8 = xb && !P->dry ? &P->w8[l] : nullptr;
+    auto Q = [&](uint8_t* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
+    auto W8 = [&](int i) -> const uint8_t* { return w8 ? w8->wr[i] : nullptr; };
+    auto X8 = [&](int i) -> const uint8_t* { return w8 ? w8->sr[i] : nullptr; };
     // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
     // fork's event itself (arm_fork before it) instead of a marker packet recorded behind it
@@ -1402,14 +1448,24 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     if (!shift || l == L - 1)  // (shifted: block l's mlp c_proj dW was queued at the end of block l+1's stage)
         ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
     if (arm && !shift) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
-    for (int c = 0; c < ch.n; ++c)
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
-                      R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
+    for (int c = 0; c < ch.n; ++c) {
+        if (xb)  // + the MX copy of dpre for the c_fc dX
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), F, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(5), nullptr, X8(5),
+                           R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F, nullptr, 0, nullptr,
+                           Q(P->dpq, c, F), Q(P->dpx, c, 4)));
+        else
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
+                          R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
+    }
     ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), 2));
     if (!shift) ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
-                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (xb)
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, F, Q(P->dpq, c, F), nullptr, Q(P->dpx, c, 4), W8(4), nullptr, X8(4),
+                           R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
+        else
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
+                          R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
         if (arm && shift) arm_fork(P, s);  // ln_2's backward: dh2, the cross c_proj dW's dY
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     }
@@ -1418,8 +1474,12 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), 4));
     if (shift) ERGM_TRY(dw_flush(P, ch));  // c_fc + cross c_proj (+ mlp c_proj in the first stage)
     for (int c = 0; c < ch.n; ++c) {
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
-                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (xb)
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(3), nullptr, X8(3),
+                           R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE, nullptr));
+        else
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
+                          R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
         if (arm && !P->capkv_split && !shift) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
         if (!P->dry) {
             const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1450,8 +1510,14 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     }
     if (!shift) ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q + caption K/V weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
-                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (xb) {
+            if (!P->dry) ERGM_TRY(quant_act(P, R(dxq, c, E), E, Tc(c), E, Q(P->gq, c, E), nullptr, Q(P->gx, c, 4), ch.s[c]));
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->gq, c, E), nullptr, Q(P->gx, c, 4), W8(2), nullptr, X8(2),
+                           R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
+        } else {
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
+                          R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        }
         if (arm && shift) arm_fork(P, s);  // ln_x's backward: dh1, the attn c_proj dW's dY
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     }
@@ -1460,8 +1526,12 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), 16));
     if (shift) ERGM_TRY(dw_flush(P, ch));  // q + attn c_proj
     for (int c = 0; c < ch.n; ++c) {
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
-                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (xb)
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(1), nullptr, X8(1),
+                           R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE, nullptr));
+        else
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
+                          R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
         if (arm && !shift) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
         if (!P->dry) {
             const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
@@ -1476,8 +1546,16 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B), 32));
     if (!shift) ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
-                      ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        if (xb) {
+            if (!P->dry)
+                ERGM_TRY(quant_act(P, R(dqkv, c, 3 * E), 3 * E, Tc(c), 3 * E, Q(P->gq, c, 3 * E), nullptr,
+                                   Q(P->gx, c, 4), ch.s[c]));
+            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, 3 * E, Q(P->gq, c, 3 * E), nullptr, Q(P->gx, c, 4), W8(0),
+                           nullptr, X8(0), R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
+        } else {
+            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
+                          ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+        }
         if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
     }

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
             if (in) {
                 *reinterpret_cast<uint32_t*>(yq + (size_t)row * ldq + c) =
                     mx_pack4(v[i].x * is, v[i].y * is, v[i].z * is, v[i].w * is);
-                if ((lane & 7) == 0) qmx[(size_t)row * ld_qmx + (c >> 5)] = (uint8_t)eb;
+                if ((lane & 7) == 0) qmx[mx_sidx(row, c >> 5, ld_qmx)] = (uint8_t)eb;
             }
         }
     } else if (yq) {  // fp8 copy for the config-5 forward GEMMs (row scale, quant.hip's scheme)
@@ -116,7 +116,8 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
                                                      float* __restrict__ part_b, int rows, int E, DropSite drop,
-                                                     int drop_res) {
+                                                     int drop_res, uint8_t* __restrict__ qmx, uint8_t* __restrict__ qmx_s,
+                                                     int ld_qs) {
     __shared__ float red[LN_WAVES_BWD][NV * 256];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 pg[NV], pb[NV], gm[NV];
@@ -202,6 +203,18 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
                     }
                     ob[0] = f2bf(u.x); ob[1] = f2bf(u.y); ob[2] = f2bf(u.z); ob[3] = f2bf(u.w);
                     *reinterpret_cast<bf16x4*>(dres_b + (size_t)row * E + c) = ob;
+                    if (qmx) {  // MX-fp8 copy of the stored bf16 values (config 5's fp8 data-gradient GEMMs): a
+                                // 32-column block is 8 consecutive lanes (E % 32 == 0, so a block is wholly in)
+                        const float w0 = bf2f(ob[0]), w1 = bf2f(ob[1]), w2 = bf2f(ob[2]), w3 = bf2f(ob[3]);
+                        float am = fmaxf(fmaxf(fabsf(w0), fabsf(w1)), fmaxf(fabsf(w2), fabsf(w3)));
+                        am = fmaxf(am, __shfl_xor(am, 1, 64));
+                        am = fmaxf(am, __shfl_xor(am, 2, 64));
+                        am = fmaxf(am, __shfl_xor(am, 4, 64));
+                        const int eb = mx_exp_biased(am);
+                        const float is = mx_inv_scale(eb);
+                        *reinterpret_cast<uint32_t*>(qmx + (size_t)row * E + c) = mx_pack4(w0 * is, w1 * is, w2 * is, w3 * is);
+                        if ((lane & 7) == 0) qmx_s[mx_sidx(row, c >> 5, ld_qs)] = (uint8_t)eb;
+                    }
                 }
             }
         }
@@ -366,7 +379,7 @@ int layernorm_fwd_ld(const float* x, const float* gamma, const float* beta, void
                      int rows, int E, float eps, hipStream_t s, void* yq, int ldq, float* qscale, void* qmx, int ld_qmx) {
     if (diag_skip() & 16) return ERGM_OK;
     ERGM_CHECK_ARG(!yq || ((qscale || qmx) && ldq >= E && ldq % 4 == 0), "layernorm_fwd: bad fp8 output");
-    ERGM_CHECK_ARG(!qmx || (E % 32 == 0 && ld_qmx >= E / 32), "layernorm_fwd: bad MX-fp8 output");
+    ERGM_CHECK_ARG(!qmx || (E % 32 == 0 && ld_qmx >= rows), "layernorm_fwd: bad MX-fp8 output");
     auto* qm = reinterpret_cast<uint8_t*>(qmx);
     auto* q8 = reinterpret_cast<uint8_t*>(yq);
     ERGM_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null argument");
@@ -422,17 +435,20 @@ int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
 
 int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
                        float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop, int drop_res) {
+                       const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs) {
     if (diag_skip() & 32) return ERGM_OK;
     ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
+    ERGM_CHECK_ARG(!qmx || (dres_bf16 && qmx_s && E % 32 == 0 && ld_qs >= rows), "layernorm_bwd: bad MX-fp8 output");
+    auto* q8 = reinterpret_cast<uint8_t*>(qmx);
+    auto* qs = reinterpret_cast<uint8_t*>(qmx_s);
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
     switch (cdiv(E, 256)) {
-        case 1: ERGM_LAUNCH(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        case 2: ERGM_LAUNCH(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        case 3: ERGM_LAUNCH(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
-        default: ERGM_LAUNCH(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res); break;
+        case 1: ERGM_LAUNCH(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
+        case 2: ERGM_LAUNCH(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
+        case 3: ERGM_LAUNCH(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
+        default: ERGM_LAUNCH(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
     }
     return check_launch("layernorm_bwd");
 }
@@ -466,7 +482,8 @@ extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* 
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
     hipStream_t s = as_stream(stream);
-    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E), 0));
+    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E), 0,
+                                 nullptr, nullptr, 0));
     return layernorm_param_reduce(pg, pb, rows, E, dgamma, dbeta, s);
 }
 

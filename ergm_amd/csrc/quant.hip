@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void mx_quant_rows_kernel(const void* __restri
         const int eb = mx_quant8_x4(v, q);
         if (c < cols) {
             *reinterpret_cast<uint2*>(Q + (size_t)row * ldq + c) = q;
-            if ((lane & 3) == 0) S[(size_t)row * lds + (c >> 5)] = (uint8_t)eb;
+            if ((lane & 3) == 0) S[mx_sidx(row, c >> 5, lds)] = (uint8_t)eb;
         }
     }
 }
@@ -277,6 +277,21 @@ __global__ __launch_bounds__(256) void mx_quant_weight_kernel(MxJobs J) {
             cm[j] = fmaxf(cm[j], fabsf(w[r][j]));
         }
     }
+    if (jb.Wr) {  // row form: a 32-column block is 8 consecutive threads (same row group kg)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float am = fmaxf(fmaxf(fabsf(w[r][0]), fabsf(w[r][1])), fmaxf(fabsf(w[r][2]), fabsf(w[r][3])));
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            am = fmaxf(am, __shfl_xor(am, 4, 64));
+            const int eb = mx_exp_biased(am);
+            const float is = mx_inv_scale(eb);
+            const size_t row = (size_t)(k0 + kq + r);
+            *reinterpret_cast<uint32_t*>(jb.Wr + row * jb.ldr + n0 + nq) =
+                mx_pack4(w[r][0] * is, w[r][1] * is, w[r][2] * is, w[r][3] * is);
+            if ((threadIdx.x & 7) == 0) jb.scr[mx_sidx((int)row, (n0 + nq) >> 5, jb.ldsr)] = (uint8_t)eb;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[kg][nq + j] = cm[j];
     __syncthreads();
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(256) void mx_quant_weight_kernel(MxJobs J) {
         for (int i = 1; i < 8; ++i) m = fmaxf(m, red[8 * h + i][n]);
         const int eb = mx_exp_biased(m);
         ebs[h][n] = eb;
-        jb.sc[(size_t)(n0 + n) * jb.lds + (k0 >> 5) + h] = (uint8_t)eb;
+        jb.sc[mx_sidx(n0 + n, (k0 >> 5) + h, jb.lds)] = (uint8_t)eb;
     }
     __syncthreads();
 #pragma unroll
@@ -309,8 +324,10 @@ int quant_weights_mx(const MxJobs& J0, hipStream_t s) {
     for (int i = 0; i < J.n; ++i) {
         MxJob& j = J.j[i];
         ERGM_CHECK_ARG(j.W && j.Wt && j.sc && j.N % 64 == 0 && j.K % 64 == 0 && j.ldt >= j.K && j.ldt % 16 == 0 &&
-                           j.ldw >= j.N && j.ldw % 4 == 0 && j.lds >= j.K / 32,
+                           j.ldw >= j.N && j.ldw % 4 == 0 && j.lds >= j.N,
                        "quant_weights_mx: bad matrix %d (K=%d N=%d)", i, j.K, j.N);
+        ERGM_CHECK_ARG(!j.Wr || (j.scr && j.ldr >= j.N && j.ldr % 4 == 0 && j.ldsr >= j.K),
+                       "quant_weights_mx: bad row-form output of matrix %d", i);
         j.blk = b;
         b += (j.N / 64) * (j.K / 64);
     }
@@ -321,7 +338,7 @@ int quant_weights_mx(const MxJobs& J0, hipStream_t s) {
 int quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
                   hipStream_t s) {
     ERGM_CHECK_ARG(X && Q && S && rows > 0 && cols > 0 && cols % 32 == 0 && ldx % 8 == 0 && ldx >= cols &&
-                       ldq >= cols && ldq % 8 == 0 && lds >= cols / 32,
+                       ldq >= cols && ldq % 8 == 0 && lds >= rows,
                    "quant_rows_mx: bad argument");
     ERGM_CHECK_ARG(x_dtype == ERGM_BF16 || x_dtype == ERGM_F32, "quant_rows_mx: bad dtype");
     dim3 grid(cdiv(rows, 4));
@@ -380,10 +397,10 @@ extern "C" int ergm_quant_rows_mx(const void* X, int x_dtype, int ldx, int rows,
 }
 
 extern "C" int ergm_quant_weight_mx(const void* W, int ldw, int K, int N, void* Wt, int ldt, void* S, int lds,
-                                    void* stream) {
+                                    void* Wr, int ldr, void* Sr, int ldsr, void* stream) {
     MxJobs J{};
     J.n = 1;
     J.j[0] = MxJob{reinterpret_cast<const __bf16*>(W), reinterpret_cast<uint8_t*>(Wt), reinterpret_cast<uint8_t*>(S), ldw,
-                   K, N, ldt, lds, 0};
+                   K, N, ldt, lds, 0, reinterpret_cast<uint8_t*>(Wr), reinterpret_cast<uint8_t*>(Sr), ldr, ldsr};
     return quant_weights_mx(J, as_stream(stream));
 }

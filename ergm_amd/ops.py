@@ -103,8 +103,10 @@ def gemm_mx(A8: torch.Tensor, a_sc: torch.Tensor, B8t: torch.Tensor, b_sc: torch
             aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0, q_out: Optional[torch.Tensor] = None,
             q_sc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """MX-fp8 GEMM: C[M,N] = epilogue(alpha · Σ_k dequant(A8)[m,k]·dequant(B8t)[n,k]) with A8 [M,K], B8t [N,K]
-    e4m3 bytes and their e8m0 block scales a_sc [M,K/32], b_sc [N,K/32] (uint8, 2^(byte-127) per 32-element K
-    block).  q_out / q_sc (BIAS_GELU): the MX copy of the bf16 output ([M,N] / [M,N/32] uint8)."""
+    e4m3 bytes and their e8m0 block scales (uint8, 2^(byte-127) per 32-element K block) in the library's
+    K-step-major layout: a_sc [K/128, pitch >= M, 4], b_sc [K/128, pitch >= N, 4] (``mx_tile`` converts a
+    [rows, K/32] array).  q_out / q_sc (BIAS_GELU / GELU_BWD): the MX copy of the bf16 output ([M,N] uint8 and
+    [N/128, pitch >= M, 4])."""
     _need_gpu(A8, B8t, a_sc, b_sc)
     M, K = A8.shape
     N = B8t.shape[0]
@@ -114,34 +116,62 @@ def gemm_mx(A8: torch.Tensor, a_sc: torch.Tensor, B8t: torch.Tensor, b_sc: torch
                    b_layout=L.NK, c_dtype=L.BF16 if out.dtype == torch.bfloat16 else L.F32, epilogue=epilogue,
                    alpha=alpha, bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
                    aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0)
-    L.check(L.load().ergm_gemm_mx(C.byref(d), _ptr(A8), _ptr(a_sc), a_sc.stride(0), _ptr(B8t), _ptr(b_sc),
-                                  b_sc.stride(0), _ptr(out), _ptr(q_out), _ptr(q_sc),
+    L.check(L.load().ergm_gemm_mx(C.byref(d), _ptr(A8), _ptr(a_sc), _pitch(a_sc), _ptr(B8t), _ptr(b_sc),
+                                  _pitch(b_sc), _ptr(out), _ptr(q_out), _ptr(q_sc),
                                   q_out.stride(0) if q_out is not None else 0,
-                                  q_sc.stride(0) if q_sc is not None else 0, _stream(A8.device)), "ergm_gemm_mx")
+                                  _pitch(q_sc) if q_sc is not None else 0, _stream(A8.device)), "ergm_gemm_mx")
     return out
 
 
+def _pitch(s: torch.Tensor) -> int:
+    """Row pitch of an MX scale array [K/128, pitch, 4] (a 2-D [rows, 4] array: one 128-deep K step)."""
+    assert s.dtype == torch.uint8 and s.is_contiguous() and s.shape[-1] == 4 and s.dim() in (2, 3)
+    return s.shape[-2]
+
+
+def mx_tile(S: torch.Tensor, pitch: Optional[int] = None) -> torch.Tensor:
+    """[rows, nb] e8m0 block scales (block b = elements 32b..32b+31 of a row) → the library layout
+    [ceil(nb/4), pitch, 4] (padding bytes 127)."""
+    rows, nb = S.shape
+    pitch = rows if pitch is None else pitch
+    out = torch.full(((nb + 3) // 4, pitch, 4), 127, dtype=torch.uint8, device=S.device)
+    Sp = torch.full((rows, out.shape[0] * 4), 127, dtype=torch.uint8, device=S.device)
+    Sp[:, :nb] = S
+    out[:, :rows] = Sp.reshape(rows, -1, 4).permute(1, 0, 2)
+    return out
+
+
+def mx_untile(T: torch.Tensor, rows: int, nb: int) -> torch.Tensor:
+    """Inverse of mx_tile: [K/128, pitch, 4] → [rows, nb]."""
+    return T[:, :rows].permute(1, 0, 2).reshape(rows, -1)[:, :nb].contiguous()
+
+
 def quant_rows_mx(X: torch.Tensor, cols: Optional[int] = None):
-    """MX-fp8 quantisation of rows: returns (Q [rows, cols] uint8 e4m3, S [rows, cols/32] uint8 e8m0)."""
+    """MX-fp8 quantisation of rows: returns (Q [rows, cols] uint8 e4m3, S [ceil(cols/128), rows, 4] uint8 e8m0 in
+    the library layout, ``mx_untile`` gives [rows, cols/32])."""
     _need_gpu(X)
     rows = X.shape[0]
     cols = X.shape[1] if cols is None else cols
     Q = torch.empty(rows, cols, dtype=torch.uint8, device=X.device)
-    S = torch.empty(rows, cols // 32, dtype=torch.uint8, device=X.device)
+    S = torch.empty((cols + 127) // 128, rows, 4, dtype=torch.uint8, device=X.device)
     dt = L.BF16 if X.dtype == torch.bfloat16 else L.F32
-    L.call("ergm_quant_rows_mx", _ptr(X), dt, X.stride(0), rows, cols, _ptr(Q), cols, _ptr(S), cols // 32,
+    L.call("ergm_quant_rows_mx", _ptr(X), dt, X.stride(0), rows, cols, _ptr(Q), cols, _ptr(S), rows,
            _stream(X.device))
     return Q, S
 
 
-def quant_weight_mx(W: torch.Tensor):
-    """Conv1D weight W [K, N] (bf16) → (Wt [N, K] e4m3 bytes, S [N, K/32] e8m0 block scales)."""
+def quant_weight_mx(W: torch.Tensor, row_form: bool = False):
+    """Conv1D weight W [K, N] (bf16) → (Wt [N, K] e4m3 bytes, S [K/128, N, 4] e8m0 block scales); with
+    ``row_form`` also (Wr [K, N], Sr [N/128, K, 4]): W's rows quantised along N (the dX GEMM's B operand)."""
     _need_gpu(W)
     K, N = W.shape
     Wt = torch.empty(N, K, dtype=torch.uint8, device=W.device)
-    S = torch.empty(N, K // 32, dtype=torch.uint8, device=W.device)
-    L.call("ergm_quant_weight_mx", _ptr(W), W.stride(0), K, N, _ptr(Wt), K, _ptr(S), K // 32, _stream(W.device))
-    return Wt, S
+    S = torch.empty((K + 127) // 128, N, 4, dtype=torch.uint8, device=W.device)
+    Wr = torch.empty(K, N, dtype=torch.uint8, device=W.device) if row_form else None
+    Sr = torch.empty((N + 127) // 128, K, 4, dtype=torch.uint8, device=W.device) if row_form else None
+    L.call("ergm_quant_weight_mx", _ptr(W), W.stride(0), K, N, _ptr(Wt), K, _ptr(S), N, _ptr(Wr), N, _ptr(Sr), K,
+           _stream(W.device))
+    return (Wt, S, Wr, Sr) if row_form else (Wt, S)
 
 
 def dropout_desc(p: float, seed: int, offset: int, site: int, row0: int = 0) -> L.Dropout:

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 6
+#define ERGM_ABI_VERSION 7
 
 typedef enum {
     ERGM_OK = 0,
@@ -162,24 +162,32 @@ int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols,
 int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K, int N, void* Wt, int ldt,
                           float* scale, void* amax_ws, void* stream);
 
-/* MX-fp8 (OCP microscaling) GEMM, config 5's forward: A [M][lda] and B [N][ldb] e4m3fn bytes (k contiguous),
+/* MX-fp8 (OCP microscaling) GEMM, config 5's forward (and, with ERGM_FP8_BWD, its data-gradient GEMMs): A [M][lda]
+ * and B [N][ldb] e4m3fn bytes (k contiguous),
  * each with an e8m0 scale byte per 32-element K block (a_scale [M][ld_sa], b_scale [N][ld_sb]: 2^(byte-127)),
  *   C = epilogue(alpha · Σ_blocks 2^(ea+eb-254) · Σ_{k in block} A[m][k]·B[n][k])
  * on v_mfma_scale_f32_16x16x128_f8f6f4 with the block scales consumed by the MFMA (no dequantisation pass).
- * K % 128 == 0, ld_sa / ld_sb >= K/32 and multiples of 4.  Epilogues as ergm_gemm_f8.  q_out / q_scale
- * (BIAS_GELU only, N % 32 == 0): the epilogue also writes the MX copy of its bf16 output, [M][ld_q] e4m3 and
+ * Scale layout (every MX scale array of this library): the 4 bytes of one row's 128-deep K step form a word and
+ * the words of one K step are contiguous over the rows — byte (row r, block b) at ((b/4)·pitch + r)·4 + b%4, with
+ * pitch >= the row count (ld_sa >= M, ld_sb >= N, ld_qs >= M), so a GEMM stage loads its scales as whole lines.
+ * K % 128 == 0.  Epilogues as ergm_gemm_f8, plus GELU_BWD (bf16 C,
+ * aux = gelu_new').  q_out / q_scale (BIAS_GELU or GELU_BWD, N % 32 == 0): the epilogue also writes the MX copy
+ * of its bf16 output, [M][ld_q] e4m3 and
  * [M][ld_qs] e8m0 (the next MX GEMM's A operand).  Tile configurations as ergm_gemm_f8 (ergm_gemm_f8_tune). */
 int ergm_gemm_mx(const ergm_gemm_desc* desc, const void* A, const void* a_scale, int ld_sa, const void* B,
                  const void* b_scale, int ld_sb, void* C, void* q_out, void* q_scale, int ld_q, int ld_qs, void* stream);
 /* MX-fp8 quantisation of rows (activations): block b of row r = columns 32b..32b+31; e = the smallest integer
- * with max|block| <= 448·2^e (0 for a zero block), S[r][b] = e + 127, Q[r][c] = e4m3(X[r][c]·2^-e) (exact
- * scaling, round to nearest even, never saturating).  X bf16 or f32 (x_dtype), cols % 32 == 0.            */
+ * with max|block| <= 448·2^e (0 for a zero block), scale byte (r, b) = e + 127 in the layout above (pitch lds >=
+ * rows), Q[r][c] = e4m3(X[r][c]·2^-e) (exact scaling, round to nearest even, never saturating).  X bf16 or f32
+ * (x_dtype), cols % 32 == 0.                                                                                  */
 int ergm_quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
                        void* stream);
 /* MX-fp8 quantisation of a Conv1D weight W [K][ldw] (bf16) into its transpose Wt [N][ldt] (k contiguous) with a
- * scale per (column n, 32-row block): S [N][lds] (lds >= K/32), same rule as ergm_quant_rows_mx; one pass, no
- * amax pass.  K, N multiples of 64.                                                                         */
-int ergm_quant_weight_mx(const void* W, int ldw, int K, int N, void* Wt, int ldt, void* S, int lds, void* stream);
+ * scale per (column n, 32-row block): S, pitch lds >= N; same rule as ergm_quant_rows_mx; one pass, no amax pass.
+ * Optionally (Wr != NULL) in the same pass the row form — Wr [K][ldr] e4m3 with a scale per (row k, 32-column
+ * block), Sr pitch ldsr >= K: the B operand of the data-gradient GEMM dX = dY·Wᵀ.  K, N multiples of 64.       */
+int ergm_quant_weight_mx(const void* W, int ldw, int K, int N, void* Wt, int ldt, void* S, int lds, void* Wr, int ldr,
+                         void* Sr, int ldsr, void* stream);
 
 /* Fused attention over head_dim = 64, token-major tensors with head h at columns [64h, 64h+64):
  *   Q[b][s][h*64+d] = q + (b*Sq + s)*ldq + h*64 + d     (likewise K/V with Sk rows, O with ldo)

@@ -4,6 +4,8 @@ import sys
 
 import torch
 
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+
 from ergm_amd import _lib as L
 from ergm_amd import ops
 
