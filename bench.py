@@ -40,8 +40,6 @@ PEAK_HBM_GBS = 8000.0
 def lmhead_split_cols(T: int, Vp: int) -> int:
     """Columns of the LM head's main launch (model.cpp lmhead_split_cols): the largest multiple of 256
     whose 256x256 tiles fill whole rounds of 256 CUs; the rest runs as a small-tile tail launch."""
-    if os.environ.get("ERGM_LMHEAD_TAIL", "1")[:1] == "0":
-        return Vp
     rows, q = -(-T // 256), 256
     while rows % 2 == 0 and q > 1:
         rows //= 2
@@ -183,6 +181,12 @@ def main():
     ap.add_argument("--torch-metrics", action="store_true",
                     help="per-step metrics with framework ops instead of the executor's loss finalisation")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
+    ap.add_argument("--fuse-optim", action="store_true",
+                    help="single process: AdamW of the block Conv1D weights inside the weight-gradient GEMM epilogues and "
+                         "of the LayerNorm parameters inside their gradient reductions (FusedAdamW(fuse=True)) instead of "
+                         "per-range passes (measured slower at C2, profiles/r04_experiments.txt)")
+    ap.add_argument("--keep-grads", action="store_true",
+                    help="with the fused optimizer, still write the fp32 gradients of the fused ranges")
     ap.add_argument("--defer-update", action="store_true",
                     help="single process: run the block updates after the backward, overlapping the next forward")
     ap.add_argument("--no-gpu-only", dest="gpu_only", action="store_false",
@@ -192,6 +196,11 @@ def main():
                     help="attn/resid/embd dropout (default: the config's 0.1, as the reference trains; 0 = off)")
     ap.add_argument("--seed", type=int, default=0, help="torch.manual_seed before the model is built (dropout masks)")
     args = ap.parse_args()
+    # every ERGM_* variable of this run is recorded in the JSON line (none changes results except the documented
+    # data-parallel exchange choices); the library has no knock-out switches, refuse a stale one
+    if "ERGM_DIAG_SKIP" in os.environ:
+        raise SystemExit("ERGM_DIAG_SKIP is not a switch of this library any more: unset it")
+    env_overrides = {k: v for k, v in sorted(os.environ.items()) if k.startswith("ERGM_") and k != "ERGM_BENCH_CHILD"}
     # the bench's data-parallel exchange: bf16 with the sharded optimizer update (library defaults: fp32 all-reduce,
     # replicated update; tests/test_dist_gloo.py bounds the bf16 trajectory against the fp32 one)
     os.environ.setdefault("ERGM_DP_GRAD", "bf16")
@@ -224,17 +233,6 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if os.environ.get("ERGM_MAIN_PRIO"):  # experiment hook: the step on a stream of the given priority (-1 high)
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=int(os.environ["ERGM_MAIN_PRIO"])))
-    if os.environ.get("ERGM_MAIN_CUMASK"):  # experiment hook: the caller's stream restricted to a CU mask
-        import ctypes as C
-        from ergm_amd import _lib
-        m = os.environ["ERGM_MAIN_CUMASK"]
-        words = [int(m[max(0, e - 8):e], 16) for e in range(len(m), 0, -8)]
-        sp = C.c_void_p()
-        if _lib._hip().hipExtStreamCreateWithCUMask(C.byref(sp), len(words), (C.c_uint32 * len(words))(*words)) != 0:
-            raise SystemExit("hipExtStreamCreateWithCUMask failed")
-        torch.cuda.set_stream(torch.cuda.ExternalStream(sp.value, device=dev))
     pg = None
     backend = None
     # host-cost hook (one-GPU box): ERGM_BENCH_FAKE_PG=N runs ONE process as rank 0 of a torch "fake" process
@@ -276,8 +274,10 @@ def main():
     torch.manual_seed(args.seed)  # the dropout mask stream (GPT2LMHeadModel draws its seed from torch's generator)
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
-    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim,
-                     defer=args.defer_update and world == 1)
+    defer = args.defer_update and world == 1
+    fuse = args.fuse_optim and world == 1 and not args.no_overlap_optim and not defer
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim, defer=defer, fuse=fuse,
+                     keep_grads=args.keep_grads or not fuse)
     if args.adamw_blocks is not None:
         opt.overlap_blocks = args.adamw_blocks
     total = args.warmup + args.steps
@@ -511,10 +511,16 @@ def main():
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S, E, Lyr, V),
                                                          0)},
-        "optimizer": "FusedAdamW " + ((f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks}), "
+        "optimizer": "FusedAdamW " + (("fused: every block's Conv1D weights + biases updated in the epilogue of the "
+                                       "weight-gradient GEMM that forms their gradient, LayerNorm parameters in their "
+                                       "gradient reduction, the rest per range overlapped with backward"
+                                       + ("" if opt.keep_grads else " (the fused ranges' fp32 gradients are not "
+                                          "materialised: the update consumes them in registers)")) if fuse else
+                                      (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks}), "
                                        + ("scheduled by the native executor" if world == 1 else
                                           "after each bucket's exchange (comm stream)"))
                                       if not args.no_overlap_optim else "after backward"),
+        "env": env_overrides,
         "world_size": world,
         "dp": {"backend": backend, "rehearsal": rehearse, "grad_comm": runner.dp.grad_comm,
                "grad_bytes_sent_per_rank_per_step": runner.dp.bytes_per_step,

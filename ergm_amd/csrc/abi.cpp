@@ -15,11 +15,6 @@ thread_local LaunchBind g_bind;  // fork point bound to the next launches (commo
 thread_local hipStream_t g_watch_s = nullptr;
 thread_local bool g_watch_dirty = true;
 
-int diag_skip() {
-    static const int v = getenv("ERGM_DIAG_SKIP") ? atoi(getenv("ERGM_DIAG_SKIP")) : 0;
-    return v;
-}
-
 void set_error(const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);

@@ -12,27 +12,16 @@
 
 namespace ergm {
 
-__device__ __forceinline__ void adamw_one(float4& pp, const float4& gg, float4& mm, float4& vv, bf16x4& ob, float decay,
-                                          float one_m_b1, float b2, float one_m_b2, float eps, float step_size,
-                                          float bc2_sqrt) {
-    // no FMA contraction: every kernel that applies this update (whole buffer, per bucket, per row
-    // selection; temporal or non-temporal memory access) must round identically
-#pragma clang fp contract(off)
+__device__ __forceinline__ void adamw_one(float4& pp, const float4& gg, float4& mm, float4& vv, bf16x4& ob,
+                                          const AdamScalars& s) {
     float* P = reinterpret_cast<float*>(&pp);
     const float* G = reinterpret_cast<const float*>(&gg);
     float* Mv = reinterpret_cast<float*>(&mm);
     float* Vv = reinterpret_cast<float*>(&vv);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        float x = P[j] * decay;
-        float mj = Mv[j] + one_m_b1 * (G[j] - Mv[j]);
-        float vj = Vv[j] * b2 + one_m_b2 * (G[j] * G[j]);
-        float denom = sqrtf(vj) / bc2_sqrt + eps;
-        x = x + (-step_size) * (mj / denom);
-        P[j] = x;
-        Mv[j] = mj;
-        Vv[j] = vj;
-        ob[j] = f2bf(x);
+        P[j] = adamw_elem(P[j], G[j], Mv[j], Vv[j], s);
+        ob[j] = f2bf(P[j]);
     }
 }
 
@@ -61,9 +50,7 @@ __device__ __forceinline__ void st4(float4* p, const float4& x) {
 template <bool NT>
 __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                     float4* __restrict__ m, float4* __restrict__ v,
-                                                    bf16x4* __restrict__ pb, size_t n4, float decay, float one_m_b1,
-                                                    float b2, float one_m_b2, float eps, float step_size,
-                                                    float bc2_sqrt) {
+                                                    bf16x4* __restrict__ pb, size_t n4, AdamScalars sc) {
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += 2 * stride) {
         const size_t i2 = i + stride;
@@ -77,13 +64,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, cons
             v1 = ld4<NT>(v + i2);
         }
         bf16x4 o0, o1;
-        adamw_one(p0, g0, m0, v0, o0, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+        adamw_one(p0, g0, m0, v0, o0, sc);
         st4<NT>(p + i, p0);
         st4<NT>(m + i, m0);
         st4<NT>(v + i, v0);
         if (pb) pb[i] = o0;
         if (two) {
-            adamw_one(p1, g1, m1, v1, o1, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+            adamw_one(p1, g1, m1, v1, o1, sc);
             st4<NT>(p + i2, p1);
             st4<NT>(m + i2, m1);
             st4<NT>(v + i2, v1);
@@ -116,22 +103,27 @@ __global__ __launch_bounds__(256) void axpy_kernel(const float4* __restrict__ x,
 __global__ __launch_bounds__(256) void adamw_rows_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v,
                                                          bf16x4* __restrict__ pb, int rows, int row4,
-                                                         const uint8_t* __restrict__ flag, int select, float decay,
-                                                         float one_m_b1, float b2, float one_m_b2, float eps,
-                                                         float step_size, float bc2_sqrt) {
+                                                         const uint8_t* __restrict__ flag, int select, AdamScalars sc) {
     for (int r = blockIdx.x; r < rows; r += gridDim.x) {
         if ((flag[r] != 0) != (select != 0)) continue;
         for (int c = threadIdx.x; c < row4; c += 256) {
             const size_t i = (size_t)r * row4 + c;
             float4 pp = p[i], gg = nt_load4(g + i), mm = m[i], vv = v[i];
             bf16x4 o;
-            adamw_one(pp, gg, mm, vv, o, decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt);
+            adamw_one(pp, gg, mm, vv, o, sc);
             p[i] = pp;
             m[i] = mm;
             v[i] = vv;
             if (pb) pb[i] = o;
         }
     }
+}
+
+AdamScalars adam_scalars(double lr, double beta1, double beta2, float eps, double weight_decay, float step_size,
+                         float bc2_sqrt) {
+    // the scalar products torch forms in double and rounds once when applied to fp32 tensors
+    return AdamScalars{(float)(1.0 - lr * weight_decay), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps,
+                       step_size, bc2_sqrt};
 }
 
 static unsigned grid_for(size_t n4) {
@@ -151,7 +143,6 @@ using namespace ergm;
 extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, size_t n, double lr,
                                double beta1, double beta2, float eps, double weight_decay, float step_size,
                                float bc2_sqrt, int max_blocks, void* stream) {
-    if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v, "adamw: null argument");
     ERGM_CHECK_ARG(max_blocks >= 0, "adamw: max_blocks must be >= 0");
     ERGM_CHECK_ARG(n % 4 == 0, "adamw: n must be a multiple of 4");
@@ -159,44 +150,30 @@ extern "C" int ergm_adamw_step(float* p, const float* g, float* m, float* v, voi
     ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw: bf16 copy alignment");
     size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
-    // the scalar products torch forms in double and rounds once when applied to fp32 tensors
-    float decay = (float)(1.0 - lr * weight_decay);
-    float one_m_b1 = (float)(1.0 - beta1);
-    float one_m_b2 = (float)(1.0 - beta2);
+    const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
     unsigned grid = grid_for2(n4);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
-    // non-temporal parameter / moment traffic: C2 +1.2 %, C5 +0.6 % (profiles/r01_overlap_experiments.txt
-    // #15); ERGM_ADAMW_NT=0 disables (A/B)
-    static const bool nt = !getenv("ERGM_ADAMW_NT") || atoi(getenv("ERGM_ADAMW_NT")) != 0;
-    if (nt)
-        ERGM_LAUNCH(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
-                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
-                           one_m_b2, eps, step_size, bc2_sqrt);
-    else
-        ERGM_LAUNCH(adamw_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p,
-                           (const float4*)g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, decay, one_m_b1, (float)beta2,
-                           one_m_b2, eps, step_size, bc2_sqrt);
+    // non-temporal parameter / moment traffic: C2 +1.2 %, C5 +0.6 % (profiles/r01_overlap_experiments.txt #15)
+    ERGM_LAUNCH(adamw_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
+                (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, sc);
     return check_launch("adamw");
 }
 
 extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, void* p_bf16, int rows, int row_len,
                                const void* row_flag, int select, double lr, double beta1, double beta2, float eps,
                                double weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
-    if (diag_skip() & 4) return ERGM_OK;
     ERGM_CHECK_ARG(p && g && m && v && row_flag, "adamw_rows: null argument");
     ERGM_CHECK_ARG(rows >= 0 && row_len > 0 && row_len % 4 == 0, "adamw_rows: row_len must be a positive multiple of 4");
     ERGM_CHECK_ARG(max_blocks >= 0, "adamw_rows: max_blocks must be >= 0");
     ERGM_CHECK_ARG(aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v), "adamw_rows: 16-byte alignment");
     ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw_rows: bf16 copy alignment");
     if (rows == 0) return ERGM_OK;
-    float decay = (float)(1.0 - lr * weight_decay);
-    float one_m_b1 = (float)(1.0 - beta1);
-    float one_m_b2 = (float)(1.0 - beta2);
+    const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
     unsigned grid = (unsigned)std::min(rows, 8192);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
     ERGM_LAUNCH(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, rows, row_len / 4, (const uint8_t*)row_flag, select,
-                       decay, one_m_b1, (float)beta2, one_m_b2, eps, step_size, bc2_sqrt);
+                       sc);
     return check_launch("adamw_rows");
 }
 

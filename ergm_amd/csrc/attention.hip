@@ -866,9 +866,8 @@ using namespace ergm;
 
 namespace {
 bool g_attn_generic = false;  // ergm_attn_tune: force the tiled kernels even for short sequences
-// ergm_attn_tune: ring stages of the tiled kernels (0: per-kernel defaults); ERGM_ATTN_NS sets the
-// initial value (A/B runs inside the step)
-int g_attn_ns = getenv("ERGM_ATTN_NS") ? atoi(getenv("ERGM_ATTN_NS")) : 0;
+// ergm_attn_tune: ring stages of the tiled kernels (0: per-kernel defaults)
+int g_attn_ns = 0;
 
 template <bool CAUSAL, int NS, bool DROP>
 void launch_tiled_fwd(dim3 grid, hipStream_t s, const AttnArgs& a) {
@@ -930,7 +929,6 @@ extern "C" int ergm_attn_fwd(const void* q, const void* k, const void* v, void* 
 int ergm::attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
                       int ldq, int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits,
                       uint8_t* qmx, uint8_t* qms, int ldqm, int qpitch, hipStream_t s) {
-    if (diag_skip() & 64) return ERGM_OK;
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && lse && ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd: bad output");
     AttnArgs a{};
@@ -955,7 +953,6 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int H, int Sq,
                              int Sk, int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv,
                              int causal, const ergm_dropout* dropout, const void* keep_bits, void* stream) {
-    if (diag_skip() & 8) return ERGM_OK;
     ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
     ERGM_CHECK_ARG(o && dout && lse && delta && dq && dk && dv, "attn_bwd: null argument");
     ERGM_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 4 == 0 && lddk % 4 == 0 && lddv % 4 == 0,

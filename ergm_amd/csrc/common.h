@@ -69,13 +69,6 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// Diagnostic knock-out switches (ERGM_DIAG_SKIP bitmask; never set in normal runs: the results are wrong):
-// 1 = weight-gradient GEMMs, 2 = LayerNorm dγ/dβ reductions, 4 = AdamW passes, 8 = attention backward,
-// 16 = LayerNorm forward (block LayerNorms), 32 = LayerNorm backward, 64 = attention forward, 128 = LM-head
-// GEMMs, 256 = cross-entropy, 512 = block forward GEMMs, 1024 = block data-gradient GEMMs, 2048 = the
-// embedding stage's caption K/V GEMMs (dW and dX over the stacked projection).
-// Used only to measure what a class of launches costs the concurrent step.
-int diag_skip();
 
 // ---- device types -----------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -170,6 +163,45 @@ __device__ __forceinline__ float gelu_new_grad(float x) {
     float t = tanhf(u);
     return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * 0.044715f * x2);
 }
+
+// ---- torch.optim.AdamW (src/main.py:68,155), single-tensor algorithm in torch's arithmetic order ----------------
+//   p *= 1 - lr·wd;  m = m + (1-β1)(g - m)  (lerp);  v = β2·v + (1-β2)·g·g  (addcmul)
+//   p += -step_size · m / (sqrt(v)/bc2_sqrt + eps)           (addcdiv)
+// One element.  No FMA contraction: every kernel that applies this update (the optimizer passes of adamw.hip, the
+// weight-gradient GEMM epilogue of gemm.hip, the LayerNorm parameter reduce of norm.hip) must round identically.
+struct AdamScalars {
+    float decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt;
+};
+__device__ __forceinline__ float adamw_elem(float p, float g, float& m, float& v, const AdamScalars& s) {
+#pragma clang fp contract(off)
+    float x = p * s.decay;
+    const float mj = m + s.one_m_b1 * (g - m);
+    const float vj = v * s.b2 + s.one_m_b2 * (g * g);
+    const float denom = sqrtf(vj) / s.bc2_sqrt + s.eps;
+    x = x + (-s.step_size) * (mj / denom);
+    m = mj;
+    v = vj;
+    return x;
+}
+// The scalar products torch forms in double and rounds once when applied to fp32 tensors.
+AdamScalars adam_scalars(double lr, double beta1, double beta2, float eps, double weight_decay, float step_size,
+                         float bc2_sqrt);
+
+// AdamW applied where a gradient is formed (GEMM epilogue, LayerNorm reduce): parameter, moments and bf16 shadow
+// at the gradient's own index (`aligned with the gradient`); g_out: also store the gradient (nullptr: don't).
+struct AdamEpi {
+    float* p;       // nullptr: no fused update
+    float* m;
+    float* v;
+    __bf16* sh;     // nullptr: no shadow
+    int write_grad;
+    AdamScalars s;
+};
+
+__device__ __forceinline__ f32x4 ld_nt4(const float* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+}
+__device__ __forceinline__ void st_nt4(float* p, f32x4 x) { __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p)); }
 
 // ---- dropout (nn.Dropout at src/model.py:142,245,266,506) -------------------------------------
 // Counter-based: the keep decision of element (row, col) of dropout site `site` in forward number

@@ -45,7 +45,8 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
-                             float* const* dgamma, float* const* dbeta, hipStream_t s);
+                             float* const* dgamma, float* const* dbeta, hipStream_t s, const float* gbase,
+                             const AdamEpi* opt);
 int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
                           const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
                           const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s);
@@ -77,8 +78,6 @@ struct LayerW8 {
     uint8_t* w[6];
     float* sc[6];
     uint8_t* sx[6];  // MX-fp8: e8m0 scale per (column, 32-row block), [N][K/32]
-    uint8_t* wr[6];  // MX-fp8 row form (fp8 data-gradient GEMMs): W [K][N] e4m3, scale per (row, 32-column block)
-    uint8_t* sr[6];  // [K][N/32]
     unsigned* amax;
     int amax_n;
 };
@@ -93,6 +92,7 @@ struct DwJob {
     float* gW;
     float* gB;
     int ldc;  // row stride of gW (N, or the stacked matrix's width for a column slice)
+    bool fuse;  // a block Conv1D: the fused optimizer updates [W; b] in the GEMM's epilogue
 };
 
 struct ergm_model_plan {
@@ -129,12 +129,6 @@ struct ergm_model_plan {
     // every activation row and weight column, consumed by the MFMA (ergm_gemm_mx); the LayerNorms and the c_fc
     // GELU epilogue write their MX copies themselves, the weights are quantised in one pass (no amax pass)
     bool mx = true;
-    // fp8 data-gradient GEMMs (config 5 with MX, ERGM_FP8_BWD): dX = dY·Wᵀ on MX operands — the LayerNorm backward
-    // writes the MX copy of the residual-branch gradient it stores (dhq / dhx), the mlp c_proj dX epilogue that of
-    // the GELU' output (dpq / dpx), the attention-backward outputs take a row pass (gq / gx); the weights' row form
-    // is quantised with their transposed forward copy.  The weight gradients stay bf16.
-    bool mxb = false;
-    uint8_t *dhq, *dhx, *dpq, *dpx, *gq, *gx;
     std::vector<LayerW8> w8;
     uint8_t *capkv8, *qa, *qf, *qcap;
     float *capkv8_s, *sa, *sf, *scap;
@@ -149,29 +143,16 @@ struct ergm_model_plan {
     // the backward's data-gradient chains likewise (bwd_forked: the second chain is running, forked
     // after the head stage and joined by the embedding stage)
     int fwd_chains, bwd_chains;
-    int dw_main;  // weight-gradient GEMM kinds run on the data-gradient stream instead of the side stream
-    bool dw_batch;  // weight-gradient GEMMs issued in pairs behind one side-stream fork (host: fewer API calls)
-    bool dw_group;  // ... and a qualifying pair as ONE grouped launch (gemm_dw_pair)
-    // ERGM_CAPKV_SPLIT=1: the caption K/V gradients per block stage instead of stacked at the end — measured
-    // 0.25 ms/step SLOWER at C2 (6.04-6.14 vs 5.80-5.83 ms, 3 interleaved rounds, profiles/r03_experiments.txt):
-    // the backward is throughput-bound on the data- and weight-gradient streams, and 12 small GEMMs on each
-    // cost more there than the two large ones at the end, where they overlap the optimizer tail
-    int capkv_split = 0;
-    int opt_lag = 2;  // ERGM_OPT_LAG: stages between a block's backward and its AdamW launch (opt_after_layer)
-    // ERGM_DW_SHIFT=1: the weight-gradient pairs are launched when their SECOND member's dY is final, half a
-    // sub-block later than the default (c_fc + cross c_proj after ln_2's backward, q + attn c_proj after ln_x's,
-    // c_attn + the next block's mlp c_proj after ln_1's), so the side stream has work while the attention
-    // backwards run alone on the data-gradient chain
-    bool dw_shift = false;
+    bool dw_group;  // weight-gradient pairs issued behind one side-stream fork run as ONE grouped launch when both
+                    // qualify (gemm_dw_pair)
+    // stages between a block's backward and its AdamW launch (opt_after_layer): 2 measured best (vs 1: C2 -0.4 %,
+    // C5 -0.6 %; 0 slower, profiles/r02_experiments.txt)
+    int opt_lag = 2;
     std::vector<DwJob> dw_pend;
     bool bwd_forked;
     hipStream_t fwd2;
     hipEvent_t ev_f2[3];
     char* scratch3;
-    // forward chains 3 and 4 (ERGM_FWD_CHAINS up to 4): their streams and (embedding done, chain done)
-    // events; their GEMMs never split K (checked), so they need no scratch of their own
-    hipStream_t fwdx[2];
-    hipEvent_t ev_fx[2][2];
     // lookups sorted by vocabulary row (computed during the training forward, used by the embedding
     // backward) and the caller's optional touched-row flags (one byte per padded vocab row)
     uint64_t* keys;
@@ -199,8 +180,7 @@ struct ergm_model_plan {
     // (and the stacked caption K/V GEMM in forward), forked/joined with events.
     hipStream_t side;
     hipEvent_t ev_fork;
-    // fork points bound to the producing launch (common.h ERGM_LAUNCH; ERGM_BIND_FORKS=0: hipEventRecord)
-    bool bind_forks = true;
+    // fork points are bound to the producing launch (common.h ERGM_LAUNCH)
     hipEvent_t pt_ev = nullptr;  // the last fork point taken on pt_s, reusable while nothing is launched there
     hipStream_t pt_s = nullptr;
     std::vector<hipEvent_t> ev_join;  // one per backward stage (L layers + head + embed)
@@ -230,11 +210,13 @@ struct ergm_model_plan {
     hipEvent_t* evl_e;
     double* evl_flops;
     int evl_n, evl_k;
-    // diagnostic knock-out class of the launches being enqueued (ERGM_DIAG_SKIP, common.h)
-    int diag_cls;
+    // launch class of the GEMMs being enqueued (LaunchClass; 1 = block forward GEMMs, list probe 6)
+    int launch_cls;
     // executor-scheduled AdamW (ergm_model_set_optimizer): descriptor copy, its ranges, the optimizer stream
     // and the main-stream marks it waits for (one per update of a step)
     bool opt_on;
+    bool opt_fuse;  // opt.fuse in effect: block Conv1D weights and LayerNorm parameters updated where their
+                    // gradients are formed (dW epilogue, LayerNorm reduce)
     ergm_adamw_desc opt;
     std::vector<int64_t> opt_ranges;
     hipStream_t opt_s;
@@ -297,7 +279,6 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->capkv8 = P->qa = P->qf = P->qcap = nullptr;
     P->capkv8_s = P->sa = P->sf = P->scap = nullptr;
     P->capkv8_x = P->xa = P->xf = P->xcap = nullptr;
-    P->dhq = P->dhx = P->dpq = P->dpx = P->gq = P->gx = nullptr;
     P->capkv_amax = nullptr;
     if (P->f8) {
         const size_t KN[6][2] = {{E, 3 * E}, {E, E}, {E, E}, {E, E}, {E, F}, {F, E}};
@@ -308,8 +289,6 @@ size_t carve(ergm_model_plan* P, char* base) {
                 w.w[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
                 w.sc[i] = c.take<float>(KN[i][1]);
                 w.sx[i] = c.take<uint8_t>(KN[i][0] / 32 * KN[i][1]);
-                w.wr[i] = c.take<uint8_t>(KN[i][0] * KN[i][1]);
-                w.sr[i] = c.take<uint8_t>(KN[i][0] * (KN[i][1] / 32));
                 na += (int)KN[i][1];
             }
             w.amax = c.take<unsigned>(na);
@@ -328,12 +307,6 @@ size_t carve(ergm_model_plan* P, char* base) {
         P->xa = c.take<uint8_t>(T * (E / 32));
         P->xf = c.take<uint8_t>(T * (F / 32));
         P->xcap = c.take<uint8_t>(T * (E / 32));
-        P->dhq = c.take<uint8_t>(T * E);
-        P->dhx = c.take<uint8_t>(T * (E / 32));
-        P->dpq = c.take<uint8_t>(T * F);
-        P->dpx = c.take<uint8_t>(T * (F / 32));
-        P->gq = c.take<uint8_t>(T * 3 * E);
-        P->gx = c.take<uint8_t>(T * (3 * E / 32));
     }
     P->Fd = d.feat_dim > 0 ? d.feat_dim : (int)E;
     P->proj = d.has_features && P->Fd != (int)E;
@@ -439,10 +412,7 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
     size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
-    if (diag_skip() & P->diag_cls) return ERGM_OK;
-    ERGM_CHECK_ARG(w == 0 || s == nullptr || (s != P->fwdx[0] && s != P->fwdx[1]),
-                   "model: split-K GEMM on forward chain 3/4 (no scratch of its own)");
-    Probe pr(P, P->diag_cls == 512 ? 6 : -1, s, 2.0 * M * N * K);
+    Probe pr(P, P->launch_cls == 1 ? 6 : -1, s, 2.0 * M * N * K);
     char* ws = (s != nullptr && s == P->side) ? P->scratch2 : (s != nullptr && s == P->fwd2) ? P->scratch3 : P->scratch;
     return ergm_gemm(&g, A, B, C, ws, P->scratch_bytes, s);
 }
@@ -455,7 +425,6 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
           const void* aux = nullptr, int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0,
           const ergm_dropout* dropout = nullptr, uint8_t* qo = nullptr, uint8_t* qox = nullptr) {
     if (P->dry) return ERGM_OK;
-    if (diag_skip() & P->diag_cls) return ERGM_OK;
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
     g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = ldc;
@@ -476,24 +445,8 @@ int quant_act(ergm_model_plan* P, const void* X, int ldx, int rows, int cols, ui
 }
 
 
-// Executor streams.  ERGM_<NAME>_CUMASK (hex, most significant digit first, bit i = logical CU i) creates the
-// stream with a CU mask (hipExtStreamCreateWithCUMask) — for experiments that keep stream classes on disjoint CUs.
-hipError_t make_stream(hipStream_t* s, const char* env) {
-    const char* m = getenv(env);
-    // ERGM_<NAME>_PRIO (same name with PRIO for CUMASK): the stream's scheduling priority (HIP: 0 low ... -1 high)
-    std::string pe(env);
-    pe.replace(pe.find("CUMASK"), 6, "PRIO");
-    if (const char* pv = getenv(pe.c_str())) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, atoi(pv));
-    if (!m || !*m) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    std::vector<uint32_t> mask;
-    const size_t n = strlen(m);
-    for (size_t end = n; end > 0;) {  // 8 hex digits per word, least significant word first
-        const size_t beg = end >= 8 ? end - 8 : 0;
-        mask.push_back((uint32_t)strtoul(std::string(m + beg, end - beg).c_str(), nullptr, 16));
-        end = beg;
-    }
-    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-}
+// Executor streams: non-blocking (they order themselves with the caller's stream through events).
+hipError_t make_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
 
 // Fork/join events order two streams of the same device: device-scope release is enough, and skipping
 // the system-scope fence avoids an L2 writeback at every record on the critical stream.
@@ -513,7 +466,7 @@ hipEvent_t stream_point(ergm_model_plan* P, hipStream_t s, hipEvent_t ev) {
 }
 // Bind the next fork point of `s` to the launches that follow on s (the stage's producer of the fork).
 void arm_fork(ergm_model_plan* P, hipStream_t s) {
-    if (!P->dry && P->bind_forks) bind_arm(s, P->ev_fork);
+    if (!P->dry) bind_arm(s, P->ev_fork);
 }
 
 // Make the side stream wait for everything issued so far on `s` (the producer of a dW GEMM's dY).
@@ -562,46 +515,69 @@ int join_side(ergm_model_plan* P, hipStream_t s, int k) {
     return hipStreamWaitEvent(s, P->ev_join[k], 0) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: stream join");
 }
 
-struct DiagClass {  // tags the GEMMs enqueued in its scope for ERGM_DIAG_SKIP (diagnostics only)
+// Tags the GEMMs enqueued in its scope with a launch class (list probe 6 times the block forward GEMMs, class 1).
+struct LaunchClass {
     ergm_model_plan* P;
     int prev;
-    DiagClass(ergm_model_plan* P_, int c) : P(P_), prev(P_->diag_cls) { P->diag_cls = c; }
-    ~DiagClass() { P->diag_cls = prev; }
+    LaunchClass(ergm_model_plan* P_, int c) : P(P_), prev(P_->launch_cls) { P->launch_cls = c; }
+    ~LaunchClass() { P->launch_cls = prev; }
 };
+
+// The fused optimizer's update of the parameters whose gradient lives at `g` (ergm_adamw_epilogue: parameter,
+// moments and shadow aligned with the gradient; ergm_model_set_optimizer's descriptor).
+ergm_adamw_epilogue adamw_at(const ergm_model_plan* P, const float* g) {
+    const ergm_adamw_desc& o = P->opt;
+    const ptrdiff_t off = g - o.grad;
+    ergm_adamw_epilogue e{};
+    e.param = o.param + off;
+    e.exp_avg = o.exp_avg + off;
+    e.exp_avg_sq = o.exp_avg_sq + off;
+    e.param_bf16 = o.param_bf16 ? reinterpret_cast<__bf16*>(o.param_bf16) + off : nullptr;
+    e.write_grad = o.keep_grads;
+    e.lr = o.lr; e.beta1 = o.beta1; e.beta2 = o.beta2; e.weight_decay = o.weight_decay;
+    e.eps = o.eps; e.step_size = o.step_size; e.bc2_sqrt = o.bc2_sqrt;
+    return e;
+}
 
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]) and its
 // bias gradient gB[N] = Σ_t dY[t][n].  With fused_bias the A operand's column M is all ones and gB == gW + M·N,
 // so one GEMM over M+1 rows writes [gW; gB] (the extra tile row runs beside the others); otherwise the GEMM
 // sums gB from the dY fragments it stages (ergm_gemm_desc.bias_grad: measured equal at C2 but +4 % step time
 // at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
-// kind: the dW's bit in dw_main (1 mlp c_proj, 2 c_fc, 4 cross c_proj, 8 cross q, 16 attn c_proj, 32 c_attn,
-// 64 caption K/V): set bits run on the (single) data-gradient stream, the rest on the side stream.
+// With the fused optimizer (P->opt_fuse, job.fuse: a block's Conv1D) the GEMM's epilogue also applies AdamW to
+// [W; b] (ergm_adamw_epilogue) instead of leaving it to a pass over the range.
 double dw_flops(const ergm_model_plan* P, const DwJob& j) { return 2.0 * j.M * j.N * P->T + (double)j.N * P->T; }
+void dw_desc(const ergm_model_plan* P, const DwJob& j, ergm_gemm_desc& g, ergm_adamw_epilogue& ae) {
+    memset(&g, 0, sizeof(g));
+    g.M = P->fused_bias ? j.M + 1 : j.M;
+    g.N = j.N; g.K = P->T; g.lda = j.lda; g.ldb = j.ldy; g.ldc = j.ldc;
+    g.a_layout = ERGM_KM; g.b_layout = ERGM_KN; g.c_dtype = ERGM_F32; g.epilogue = ERGM_EPI_NONE;
+    g.alpha = 1.0f;
+    g.bias_grad = P->fused_bias ? nullptr : j.gB;
+    if (j.fuse && P->opt_fuse && !P->dry) {
+        ae = adamw_at(P, j.gW);
+        g.adamw = &ae;
+    }
+}
 int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
-    const int T = P->T;
-    DiagClass dc(P, 0);
     Probe pr(P, 5, s, dw_flops(P, j));
-    if (P->fused_bias)
-        return gemm(P, s, j.M + 1, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.ldc, ERGM_F32, ERGM_EPI_NONE);
-    return gemm(P, s, j.M, j.N, T, j.A, j.lda, ERGM_KM, j.dY, j.ldy, ERGM_KN, j.gW, j.ldc, ERGM_F32, ERGM_EPI_NONE,
-                nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, j.gB);
+    ergm_gemm_desc g;
+    ergm_adamw_epilogue ae;
+    dw_desc(P, j, g, ae);
+    const size_t w = ergm_gemm_workspace_size(&g);
+    ERGM_TRY(ws_need(P, w));
+    if (P->dry) return ERGM_OK;
+    return ergm_gemm(&g, j.A, j.dY, j.gW, s == P->side ? P->scratch2 : P->scratch, P->scratch_bytes, s);
 }
 // Two pending weight-gradient GEMMs as ONE grouped launch (gemm_dw_pair) when they plan to the same unsplit
 // configuration: each alone has fewer tiles than the chip has CUs (ERGM_DW_GROUP=0: two launches).
 // Returns ERGM_EUNSUPPORTED when the pair does not qualify (nothing launched).
 int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJob& j1) {
     if (!P->dw_group) return ERGM_EUNSUPPORTED;
-    const int T = P->T;
     ergm_gemm_desc g[2];
-    const DwJob* j[2] = {&j0, &j1};
-    for (int i = 0; i < 2; ++i) {
-        memset(&g[i], 0, sizeof(g[i]));
-        g[i].M = P->fused_bias ? j[i]->M + 1 : j[i]->M;
-        g[i].N = j[i]->N; g[i].K = T; g[i].lda = j[i]->lda; g[i].ldb = j[i]->ldy; g[i].ldc = j[i]->ldc;
-        g[i].a_layout = ERGM_KM; g[i].b_layout = ERGM_KN; g[i].c_dtype = ERGM_F32; g[i].epilogue = ERGM_EPI_NONE;
-        g[i].alpha = 1.0f;
-        g[i].bias_grad = P->fused_bias ? nullptr : j[i]->gB;
-    }
+    ergm_adamw_epilogue ae[2];
+    dw_desc(P, j0, g[0], ae[0]);
+    dw_desc(P, j1, g[1], ae[1]);
     const ergm_gemm_desc* d[2] = {&g[0], &g[1]};
     const void* A[2] = {j0.A, j1.A};
     const void* B[2] = {j0.dY, j1.dY};
@@ -610,17 +586,14 @@ int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJ
     Probe pr(P, 5, s, dw_flops(P, j0) + dw_flops(P, j1));
     return gemm_dw_pair(d, A, B, C, s, true);
 }
+// Queue a weight-gradient GEMM; dw_flush launches the queue on the side stream behind ONE fork from the data-
+// gradient chain(s).  fuse: a block Conv1D whose update the fused optimizer applies in the epilogue.
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
-            float* gW, float* gB, int kind = 0, int ldc = 0) {
-    const bool on_main = (P->dw_main & kind) && ch.n == 1;
-    if (!P->dry && (diag_skip() & 1)) return ERGM_OK;
-    const DwJob j{M, N, A, lda, dY, ldy, gW, gB, ldc ? ldc : N};
-    if (!on_main && P->dw_batch && !P->dry) {  // launched by the next dw_flush, behind one fork
-        P->dw_pend.push_back(j);
-        return ERGM_OK;
-    }
-    if (!on_main) ERGM_TRY(fork_side(P, ch));
-    return dw_launch(P, (P->dry || on_main) ? ch.s[0] : P->side, j);
+            float* gW, float* gB, bool fuse, int ldc = 0) {
+    const DwJob j{M, N, A, lda, dY, ldy, gW, gB, ldc ? ldc : N, fuse};
+    if (P->dry) return dw_launch(P, ch.s[0], j);
+    P->dw_pend.push_back(j);
+    return ERGM_OK;
 }
 // Launch the pending weight-gradient GEMMs on the side stream behind ONE fork from the data-gradient
 // chain(s) (every dY they read is complete there): one event record + wait instead of one per GEMM.
@@ -654,10 +627,8 @@ int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* 
     // itself goes through the embedding dropout (src/model.py:506), folded into this pass.
     const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
     const int fin = slot == 0;
-    const bool q = !fin && P->f8 && P->mx && P->mxb;  // the MX copy for the fp8 data-gradient GEMM that reads dh_b
     return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
-                              pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin, q ? P->dhq + o : nullptr,
-                              q ? P->dhx + (size_t)r0 * 4 : nullptr, T);
+                              pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin, nullptr, nullptr, T);
 }
 int ln_reduce_add(ergm_model_plan* P, int slot, float* dgamma, float* dbeta) {
     if (P->dry) return ERGM_OK;
@@ -674,16 +645,21 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
     return ln_reduce_add(P, slot, dgamma, dbeta);
 }
 
+// With the fused optimizer the reduce also applies AdamW to γ / β from their final gradients (the LayerNorm's own
+// backward, the only reader of γ in the backward, has run: the reduce is forked behind it).
 int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
     if (P->dry || P->ln_pending == 0) return ERGM_OK;
-    if (diag_skip() & 2) {
-        P->ln_pending = 0;
-        return ERGM_OK;
-    }
     ERGM_TRY(fork_side(P, ch));
     const int n = P->ln_pending;
     P->ln_pending = 0;
-    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
+    AdamEpi ae{};
+    if (P->opt_fuse) {
+        const ergm_adamw_desc& o = P->opt;
+        ae = AdamEpi{o.param, o.exp_avg, o.exp_avg_sq, reinterpret_cast<__bf16*>(o.param_bf16), o.keep_grads,
+                     adam_scalars(o.lr, o.beta1, o.beta2, o.eps, o.weight_decay, o.step_size, o.bc2_sqrt)};
+    }
+    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side,
+                                    P->opt.grad, P->opt_fuse ? &ae : nullptr);
 }
 
 
@@ -711,12 +687,6 @@ int quant_layer_weights(ergm_model_plan* P, int l, hipStream_t ss) {
         J.n = 6;
         for (int i = 0; i < 6; ++i) {
             J.j[i] = MxJob{LB(P, l, tens[i]), w.w[i], w.sx[i], N[i], K[i], N[i], K[i], N[i], 0};
-            if (P->mxb) {  // + the row form for the fp8 data-gradient GEMMs
-                J.j[i].Wr = w.wr[i];
-                J.j[i].scr = w.sr[i];
-                J.j[i].ldr = N[i];
-                J.j[i].ldsr = K[i];
-            }
         }
         ERGM_TRY(quant_weights_mx(J, ss));
         return hipEventRecord(P->ev_wq[l], ss) == hipSuccess ? ERGM_OK : fail(ERGM_EHIP, "model: event record");
@@ -803,48 +773,27 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->side = nullptr;
     P->ev_fork = nullptr;
     P->ev_join.assign(d.n_layer + 3, nullptr);
-    bool ok = make_stream(&P->side, "ERGM_SIDE_CUMASK") == hipSuccess &&
+    bool ok = make_stream(&P->side) == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     // forward chains over batch slices (1..4; ERGM_FWD_CHAINS, A/B measurements)
     P->fwd_chains = 2;
-    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = std::max(1, std::min(4, atoi(e)));
+    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = std::max(1, std::min(2, atoi(e)));
     // two backward chains measured slower at C2 (6.27 vs 5.85 ms/step: the GPU is already throughput-
     // saturated and the host enqueue grows, profiles/r02_bwd_chains_ab.txt): ERGM_BWD_CHAINS=2 enables
     P->bwd_chains = 1;
     if (const char* e = getenv("ERGM_BWD_CHAINS")) P->bwd_chains = atoi(e);
-    P->dw_main = 0;
-    if (const char* e = getenv("ERGM_DW_MAIN")) P->dw_main = atoi(e);
-    P->dw_batch = true;
-    if (const char* e = getenv("ERGM_DW_BATCH")) P->dw_batch = atoi(e) != 0;
-    if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
-    if (const char* e = getenv("ERGM_DW_SHIFT")) P->dw_shift = atoi(e) != 0;
     if (const char* e = getenv("ERGM_FP8_MX")) P->mx = atoi(e) != 0;
-    // fp8 data-gradient GEMMs: opt-in (ERGM_FP8_BWD=1).  Measured at C5 (tools/r3_mxb.sh): 1373-1381 utt/s vs
-    // 1419-1421 with the bf16 backward — the f32-output dX GEMMs run 2.2x faster in-step, but the GELU' dX, the
-    // row passes over the attention gradients and the weights' second (row-form) copy cost more than that
-    P->mxb = false;
-    if (const char* e = getenv("ERGM_FP8_BWD")) P->mxb = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
     if (const char* e = getenv("ERGM_DW_GROUP")) P->dw_group = atoi(e) != 0;
-    if (const char* e = getenv("ERGM_OPT_LAG")) P->opt_lag = std::max(0, atoi(e));
-    if (const char* e = getenv("ERGM_CAPKV_SPLIT")) P->capkv_split = atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
     for (auto& e : P->ev_f2) e = nullptr;
-    ok = ok && make_stream(&P->fwd2, "ERGM_FWD2_CUMASK") == hipSuccess;
+    ok = ok && make_stream(&P->fwd2) == hipSuccess;
     for (auto& e : P->ev_f2) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
-    for (int c = 0; c < 2; ++c) {
-        P->fwdx[c] = nullptr;
-        P->ev_fx[c][0] = P->ev_fx[c][1] = nullptr;
-        if (P->fwd_chains > 2 + c) {
-            ok = ok && hipStreamCreateWithFlags(&P->fwdx[c], hipStreamNonBlocking) == hipSuccess;
-            for (auto& e : P->ev_fx[c]) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
-        }
-    }
     P->ev_wq.assign(P->f8 ? d.n_layer : 0, nullptr);
     for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
@@ -857,7 +806,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->ln_pending = 0;
     // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py lays the
     // flat buffers out that way) and a ones column in the activations (set here; producers write columns
-    // < E / < F only); ERGM_FUSED_BIAS=0 selects the in-GEMM column sums.
+    // < E / < F only); other layouts take the in-GEMM column sums (ergm_gemm_desc.bias_grad).
     {
         const int64_t E = d.n_embd, F = d.n_inner;
         const int64_t* o = P->p.layer_off;
@@ -866,7 +815,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
                         follows(ERGM_T_XQ_W, ERGM_T_XQ_B, E, E) && follows(ERGM_T_XPROJ_W, ERGM_T_XPROJ_B, E, E) &&
                         follows(ERGM_T_FC_W, ERGM_T_FC_B, E, F) && follows(ERGM_T_MPROJ_W, ERGM_T_MPROJ_B, F, E) &&
                         P->p.g_capkv_b == P->p.g_capkv_w + E * P->L2E;
-        if (const char* e = getenv("ERGM_FUSED_BIAS")) P->fused_bias = P->fused_bias && atoi(e) != 0;
         int rc = ERGM_OK;
         for (int l = 0; l < d.n_layer && rc == ERGM_OK; ++l) {
             LayerActs& a = P->la[l];
@@ -888,8 +836,9 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->lookup_compact = nullptr;
     P->n_valid = nullptr;
     P->probe = 0;
-    P->diag_cls = 0;
+    P->launch_cls = 0;
     P->opt_on = false;
+    P->opt_fuse = false;
     P->opt_s = nullptr;
     P->opt_k = 0;
     P->ev_begin = P->ev_end = nullptr;
@@ -917,14 +866,6 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
     if (P->fwd2) {
         hipStreamSynchronize(P->fwd2);
         hipStreamDestroy(P->fwd2);
-    }
-    for (int c = 0; c < 2; ++c) {
-        for (auto e : P->ev_fx[c])
-            if (e) hipEventDestroy(e);
-        if (P->fwdx[c]) {
-            hipStreamSynchronize(P->fwdx[c]);
-            hipStreamDestroy(P->fwdx[c]);
-        }
     }
     if (P->opt_s) {
         hipStreamSynchronize(P->opt_s);
@@ -1046,7 +987,7 @@ namespace {
 // cross-attention, cross c_proj, LN2, c_fc, mlp c_proj) so that the caller can interleave the chains
 // launch by launch; -1 issues the whole block.
 int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part = -1) {
-    DiagClass dc(P, 512);
+    LaunchClass lc(P, 1);
     auto on = [part](int k) { return part < 0 || part == k; };
     if (on(0)) ERGM_TRY(wait_update(P, l, s));  // a deferred optimizer update of this block's parameters
     const ergm_model_dims& d = P->d;
@@ -1172,13 +1113,7 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
 // LM-head column split: the vocabulary-wide GEMM runs 256x256 tiles, one per CU per round; the leading
 // n0 columns are the largest multiple of 256 whose tile count fills whole rounds of 256 CUs, the
 // remaining columns (the partial last round) run as a second, small-tile GEMM spread over all CUs.
-// ERGM_LMHEAD_TAIL=0 keeps the single launch.
 int lmhead_split_cols(int T, int Vp) {
-    static const bool on = [] {
-        const char* e = getenv("ERGM_LMHEAD_TAIL");
-        return !(e && e[0] == '0');
-    }();
-    if (!on) return Vp;
     const int rows = (T + 255) / 256;
     int q = 256;  // column tiles per whole number of rounds: 256 / gcd(rows, 256)
     for (int r = rows; r % 2 == 0 && q > 1; r /= 2) q /= 2;
@@ -1212,12 +1147,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     // Two concurrent chains over the two halves of the batch (main stream: rows of batch [0, B0);
     // P->fwd2: [B0, B)): the forward is a serial chain of mostly latency-bound kernels, and a second
     // independent chain fills the CUs the first leaves idle.  nchain = 1 when B = 1 (or disabled).
-    const int nchain = std::max(1, std::min(std::min(P->fwd_chains, B), P->dry ? 2 : 4));
-    int bsplit[5];
+    const int nchain = std::max(1, std::min(P->fwd_chains, B));
+    int bsplit[3];
     for (int c = 0; c <= nchain; ++c) bsplit[c] = c * B / nchain;
-    hipStream_t cs[4] = {s, P->dry ? s : P->fwd2, P->dry ? s : P->fwdx[0], P->dry ? s : P->fwdx[1]};
-    hipEvent_t ev_emb[4] = {nullptr, P->ev_f2[1], P->ev_fx[0][0], P->ev_fx[1][0]};
-    hipEvent_t ev_done[4] = {nullptr, P->ev_f2[2], P->ev_fx[0][1], P->ev_fx[1][1]};
+    hipStream_t cs[2] = {s, P->dry ? s : P->fwd2};
+    hipEvent_t ev_emb[2] = {nullptr, P->ev_f2[1]};
+    hipEvent_t ev_done[2] = {nullptr, P->ev_f2[2]};
     auto embed = [&](int c) -> int {
         if (P->dry) return ERGM_OK;
         const int b0 = bsplit[c], nb = bsplit[c + 1] - b0;
@@ -1282,31 +1217,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                 ERGM_TRY(quant_layer_weights(P, l, ss));
             }
     }
-    // Enqueue order: launch by launch, alternating chains (ERGM_FWD_INTERLEAVE=0: block by block).  The
-    // forward's kernels are short, so the host's enqueue pace can set the GPU's: enqueued a block at a
-    // time, the chains ran one block after the other instead of side by side.
-    static const bool interleave = [] {
-        const char* e = getenv("ERGM_FWD_INTERLEAVE");
-        return !(e && e[0] == '0');
-    }();
-    // ERGM_FWD_LAG = k: chain c is enqueued c·k launches behind chain 0 (the chains' kernel types then differ at
-    // any moment: one chain's GEMM beside the other's attention / LayerNorm)
-    static const int lag = [] {
-        const char* e = getenv("ERGM_FWD_LAG");
-        return e ? std::max(0, atoi(e)) : 0;
-    }();
+    // Enqueue order: launch by launch, alternating chains.  The forward's kernels are short, so the host's enqueue
+    // pace can set the GPU's: enqueued a block at a time, the chains ran one block after the other instead of side
+    // by side (profiles/r01_overlap_experiments.txt).
     constexpr int NP = 11;  // fwd_block parts
-    if (interleave && nchain > 1) {
-        for (int g = 0; g < L * NP + (nchain - 1) * lag; ++g)
-            for (int c = 0; c < nchain; ++c) {
-                const int gc = g - c * lag;
-                if (gc < 0 || gc >= L * NP) continue;
-                ERGM_TRY(fwd_block(P, gc / NP, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], gc % NP));
-            }
-    } else {
-        for (int l = 0; l < L; ++l)
-            for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, l, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c]));
-    }
+    for (int g = 0; g < L * NP; ++g)
+        for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, g / NP, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], g % NP));
     for (int c = 1; c < nchain && !P->dry; ++c)
         if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
             return fail(ERGM_EHIP, "model: chain join");
@@ -1315,7 +1231,6 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
     {
         const int n0 = lmhead_split_cols(T, d.vocab_pad);
-        DiagClass dc(P, 128);
         {
             Probe pr(P, 1, s);  // the bench's roofline kernel: the whole-round main launch
             ERGM_TRY(gemm(P, s, T, n0, E, P->lnf, E, ERGM_MK, p.wte_b, E, ERGM_NK, logits, d.vocab_pad,
@@ -1374,7 +1289,6 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     // dh_f = dlogits · wte (contraction over the padded vocab) on the main chain; the tied-weight
     // gradient dwte = dlogitsᵀ · ln_f(h) on the side stream (joined before the embedding backward adds
     // the lookup gradients into the same buffer).
-    DiagClass dc(P, 128);
     // a caller's gradient on the returned logits (src/model.py:698 returns differentiable logits): added to the
     // cross-entropy's dlogits, scaled by the loss gradient there, so the LM-head GEMMs run with alpha 1
     const float* lm_scale = gscale;
@@ -1393,7 +1307,7 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
         hipStream_t ss = P->dry ? s : P->side;
         Probe pr(P, 3, ss);
         Probe pr5(P, 5, ss, 2.0 * Vp * E * T);
-        if (!(diag_skip() & 1)) ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
+        ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
                       ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, lm_scale));
         ERGM_TRY(side_mark(P, L + 1));
     }
@@ -1409,7 +1323,6 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
 }
 
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
-    DiagClass dc(P, 1024);
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, H = d.n_head, S = d.seq, L2E = P->L2E;
     const int L = d.n_layer;
@@ -1430,57 +1343,40 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     __bf16* dpre = P->dpre[l];
     __bf16* dxq = P->dxq[l];
     __bf16* dqkv = P->dqkv[l];
-    // per-chain row offset helpers (dry run: pointers stay null)
+    // per-chain row offset helper (dry run: pointers stay null)
     auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
     auto Tc = [&](int c) { return ch.nb[c] * S; };
-    auto lnrow = [&](const float* p, int c) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S; };
-    // fp8 data-gradient GEMMs (P->mxb): MX operands of dY (chain rows) and of the weights' row form
-    const bool xb = P->f8 && P->mx && P->mxb;
-    const LayerW8* w8 = xb && !P->dry ? &P->w8[l] : nullptr;
-    auto Q = [&](uint8_t* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
-    auto W8 = [&](int i) -> const uint8_t* { return w8 ? w8->wr[i] : nullptr; };
-    auto X8 = [&](int i) -> const uint8_t* { return w8 ? w8->sr[i] : nullptr; };
-    // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
+    // Weight-gradient pairs (mlp c_proj + c_fc, cross c_proj + q, attn c_proj + c_attn) are forked to the side
+    // stream once the dY of the second member is formed.  With the fused optimizer their epilogues rewrite the
+    // weights' bf16 shadow, so the fork comes after the second member's data-gradient GEMM instead — the last
+    // reader of that shadow in this backward (the first member's is already behind the fork point).
+    const bool late = P->opt_fuse;
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
     // fork's event itself (arm_fork before it) instead of a marker packet recorded behind it
     const bool arm = ch.n == 1 && !P->dry;
-    const bool shift = P->dw_shift && !P->capkv_split && P->dw_batch;
-    if (!shift || l == L - 1)  // (shifted: block l's mlp c_proj dW was queued at the end of block l+1's stage)
-        ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), 1));
-    if (arm && !shift) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
+    // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
+    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), true));
+    if (arm && !late) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
+    for (int c = 0; c < ch.n; ++c)
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
+                      R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
+    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), true));
+    if (!late) ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        if (xb)  // + the MX copy of dpre for the c_fc dX
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), F, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(5), nullptr, X8(5),
-                           R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F, nullptr, 0, nullptr,
-                           Q(P->dpq, c, F), Q(P->dpx, c, 4)));
-        else
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
-                          R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
+        if (arm && late) arm_fork(P, s);  // the c_fc dX: the last reader of W_fc
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
+                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
     }
-    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), 2));
-    if (!shift) ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
-    for (int c = 0; c < ch.n; ++c) {
-        if (xb)
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, F, Q(P->dpq, c, F), nullptr, Q(P->dpx, c, 4), W8(4), nullptr, X8(4),
-                           R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
-        else
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
-                          R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-        if (arm && shift) arm_fork(P, s);  // ln_2's backward: dh2, the cross c_proj dW's dY
+    if (late) ERGM_TRY(dw_flush(P, ch));
+    for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
-    }
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), 4));
-    if (shift) ERGM_TRY(dw_flush(P, ch));  // c_fc + cross c_proj (+ mlp c_proj in the first stage)
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
-        if (xb)
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(3), nullptr, X8(3),
-                           R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE, nullptr));
-        else
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
-                          R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm && !P->capkv_split && !shift) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
+                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
         if (!P->dry) {
             const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
             __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1491,48 +1387,23 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), 8));
-    if (P->capkv_split) {
-        // this block's slice of the stacked caption K/V projection: its weight gradient (columns
-        // [2El, 2E(l+1)) of [g_capkv_w; g_capkv_b]) joins the block's side-stream dW work, and the caption
-        // gradient dcap accumulates dKV_l·W_lᵀ on the data-gradient chain(s), so neither is left for the
-        // embedding stage at the end of the backward
-        DiagClass dcx(P, 2048);
-        const ergm_model_params& p = P->p;
-        const size_t co = (size_t)l * 2 * E;
-        const __bf16* dkv = P->dry ? nullptr : P->dkv_all + co;
-        ERGM_TRY(dw_gemm(P, ch, E, 2 * E, P->cap, P->XE, dkv, L2E, P->dry ? nullptr : p.g_capkv_w + co,
-                         P->dry ? nullptr : p.g_capkv_b + co, 64, L2E));
-        for (int c = 0; c < ch.n; ++c)
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 2 * E, R(dkv, c, L2E), L2E, ERGM_MK,
-                          P->dry ? nullptr : reinterpret_cast<const __bf16*>(p.capkv_w_b) + co, L2E, ERGM_NK, R(P->dcap, c, E), E, ERGM_F32,
-                          l == L - 1 ? ERGM_EPI_NONE : ERGM_EPI_ACCUM));
-    }
-    if (!shift) ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q + caption K/V weight gradients
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), true));
+    if (!late) ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        if (xb) {
-            if (!P->dry) ERGM_TRY(quant_act(P, R(dxq, c, E), E, Tc(c), E, Q(P->gq, c, E), nullptr, Q(P->gx, c, 4), ch.s[c]));
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->gq, c, E), nullptr, Q(P->gx, c, 4), W8(2), nullptr, X8(2),
-                           R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
-        } else {
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
-                          R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-        }
-        if (arm && shift) arm_fork(P, s);  // ln_x's backward: dh1, the attn c_proj dW's dY
-        ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
+        if (arm && late) arm_fork(P, s);  // the q dX: the last reader of W_q
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
+                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
     }
+    if (late) ERGM_TRY(dw_flush(P, ch));
+    for (int c = 0; c < ch.n; ++c)
+        ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), 16));
-    if (shift) ERGM_TRY(dw_flush(P, ch));  // q + attn c_proj
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
-        if (xb)
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, E, Q(P->dhq, c, E), nullptr, Q(P->dhx, c, 4), W8(1), nullptr, X8(1),
-                           R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE, nullptr));
-        else
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
-                          R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm && !shift) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
+                      R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
+        if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
         if (!P->dry) {
             const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
             const size_t bhs = (size_t)ch.b0[c] * H * S;
@@ -1543,32 +1414,20 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    3 * E, 3 * E, 1, &dp, attn_bits(P, l, 0, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B), 32));
-    if (!shift) ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
+    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B),
+                     true));
+    if (!late) ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c) {
-        if (xb) {
-            if (!P->dry)
-                ERGM_TRY(quant_act(P, R(dqkv, c, 3 * E), 3 * E, Tc(c), 3 * E, Q(P->gq, c, 3 * E), nullptr,
-                                   Q(P->gx, c, 4), ch.s[c]));
-            ERGM_TRY(gemm8(P, ch.s[c], Tc(c), E, 3 * E, Q(P->gq, c, 3 * E), nullptr, Q(P->gx, c, 4), W8(0),
-                           nullptr, X8(0), R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE, nullptr));
-        } else {
-            ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
-                          ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-        }
+        if (arm && late) arm_fork(P, s);  // the c_attn dX: the last reader of W_qkv
+        ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
+                      ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+    }
+    if (late) ERGM_TRY(dw_flush(P, ch));
+    for (int c = 0; c < ch.n; ++c) {
         if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
     }
     ERGM_TRY(ln_reduce_add(P, 3 * l, LG(P, l, ERGM_T_LN1_W), LG(P, l, ERGM_T_LN1_B)));
-    if (shift) {  // c_attn + the next stage's mlp c_proj (its dY is this stage's last output, dh0 = block l-1's dh3)
-        if (l > 0) {
-            const LayerActs an = P->dry ? LayerActs{} : P->la[l - 1];
-            ERGM_TRY(dw_gemm(P, ch, F, E, an.act, P->XF, dh0, E, LG(P, l - 1, ERGM_T_MPROJ_W),
-                             LG(P, l - 1, ERGM_T_MPROJ_B), 1));
-        }
-        ERGM_TRY(dw_flush(P, ch));
-    }
-    (void)lnrow;
     // side-stream dW GEMMs of this block are marked; the caller's stream waits (one block late) for
     // those of the block differentiated before, so block l+1's gradients are final on return.
     ERGM_TRY(ln_reduce_flush(P, ch));  // this block's three LayerNorms (+ ln_f after the head stage)
@@ -1608,16 +1467,15 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
                 return fail(ERGM_EHIP, "model: memset");
         }
     }
-    if (!P->capkv_split) {  // stacked: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main), one GEMM each
-        DiagClass dc(P, 2048);
+    {  // the stacked caption K/V projection: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main), one GEMM each
+        // (per block instead, in the block stages: 0.25 ms/step slower at C2, profiles/r03_experiments.txt #6)
         const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
-        ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, 64));
+        ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, false));
         ERGM_TRY(dw_flush(P, one));
         ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                       ERGM_EPI_NONE));
     }
-    // (split: the block stages issued them, dW per block on the side stream, dcap on the chains); mark the
-    // side stream's caption / projection work
+    // mark the side stream's caption / projection work
     ERGM_TRY(side_mark(P, L + 2));
     if (P->dry) return ERGM_OK;
     // the LM-head dwte (side stream, marked L+1) is final before the lookup gradients are added to it;
@@ -1636,6 +1494,7 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
     ERGM_CHECK_ARG(P, "model_set_optimizer: null plan");
     if (!o) {
         P->opt_on = false;
+        P->opt_fuse = false;
         return ERGM_OK;
     }
     const int L = P->d.n_layer;
@@ -1646,8 +1505,13 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
                            o->ranges[2 * k] % 4 == 0 && o->ranges[2 * k + 1] % 4 == 0,
                        "model_set_optimizer: range %d must be non-empty, 4-element aligned", k);
     ERGM_CHECK_ARG(o->wte_begin >= 0 && o->wte_begin % 4 == 0, "model_set_optimizer: bad wte_begin");
+    ERGM_CHECK_ARG(!o->fuse || (!o->defer && P->fused_bias && aligned16(o->param) && aligned16(o->exp_avg) &&
+                                aligned16(o->exp_avg_sq) && aligned16(o->grad) &&
+                                (!o->param_bf16 || aligned16(o->param_bf16))),
+                   "model_set_optimizer: fuse needs defer = 0, every Conv1D bias right after its weight and 16-byte "
+                   "aligned buffers");
     if (!P->opt_s) {
-        if (make_stream(&P->opt_s, "ERGM_OPT_CUMASK") != hipSuccess)
+        if (make_stream(&P->opt_s) != hipSuccess)
             return fail(ERGM_EHIP, "model_set_optimizer: stream creation");
         P->ev_opt.assign(L + 4, nullptr);
         for (auto& e : P->ev_opt)
@@ -1661,6 +1525,7 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
     P->opt_ranges.assign(o->ranges, o->ranges + 2 * (L + 1));
     P->opt.ranges = P->opt_ranges.data();
     P->opt_on = true;
+    P->opt_fuse = o->fuse != 0;
     return ERGM_OK;
 }
 
@@ -1698,11 +1563,19 @@ int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
     const int L = P->d.n_layer, i = L - 1 - l;
     // Block m's bucket (L-1-m) is final with its weight-gradient mark m (recorded after the LayerNorm reduce,
     // which waited for the stage's last LayerNorm backward, so the stage has read the old weights).  Its AdamW
-    // is launched `lag` stages later (ERGM_OPT_LAG, default 2): the update then overlaps later blocks' backward
+    // is launched `lag` stages later (opt_lag = 2): the update then overlaps later blocks' backward
     // instead of competing with its own block's weight-gradient GEMMs (bench A/B: lag 2 vs 1 C2 -0.4 %, C5
     // -0.6 %, C4 equal; lag 0 slower).
     const int lag = P->opt_lag;
     auto upd = [&](int m) -> int {
+        if (P->opt_fuse) {
+            // fused: a block's Conv1D weights and LayerNorm parameters (ln_f's too) were updated where their gradients
+            // were formed; of bucket 0 (head + block L-1) the emotion head is left
+            if (m != L - 1) return ERGM_OK;
+            ERGM_TRY(opt_wait(P, s, m));
+            const int64_t a = P->p.g_emo_w - P->opt.grad;
+            return opt_range(P, a, a + (int64_t)7 * P->d.n_embd);
+        }
         ERGM_TRY(opt_wait(P, s, m));
         return opt_range(P, P->opt.ranges[2 * (L - 1 - m)], P->opt.ranges[2 * (L - 1 - m) + 1]);
     };

@@ -109,12 +109,14 @@ class DPSync:
                 self._midx[key] = None
             else:
                 i, o = torch.cat(idx), torch.cat(own)
-                self._midx[key] = (i.to(self._master.device), o.to(self._master.device, self._master.dtype))
+                self._midx[key] = (i.to(self._master.device), o.to(self._master.device))
         ent = self._midx[key]
         if ent is None:
             return
         idx, own = ent
-        vals = self._master[idx] * own
+        # non-owners contribute exact zeros (a select, not a product: a non-finite value on a non-owner must not
+        # reach the owner's element through the SUM)
+        vals = torch.where(own, self._master[idx], 0.0)
         self.bytes_per_step += 2 * (self.world - 1) * vals.numel() * 4 // self.world
         if vals.is_cuda:
             dist.all_reduce(vals, group=self.pg, async_op=True).wait()

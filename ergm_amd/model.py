@@ -49,30 +49,42 @@ from .params import build_layout, state_dict_names
 from .runtime import ModelRunner
 
 
+class _LazyLogits:
+    """Descriptor of ``CausalLMOutputWithEmotionClassification.logits`` (a dataclass field): a value given to the
+    constructor (``logits=...``, as the reference builds it) is returned as is; otherwise the fp32 cast of
+    ``logits_bf16`` is made on first access, so a training step that never reads the logits pays nothing."""
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return None  # the field's default
+        v = obj.__dict__.get("_logits32")
+        if v is None and obj.__dict__.get("logits_bf16") is not None:
+            v = obj.logits_bf16.float()
+            obj.__dict__["_logits32"] = v
+        return v
+
+    def __set__(self, obj, value):
+        obj.__dict__["_logits32"] = value
+
+
 @dataclass
 class CausalLMOutputWithEmotionClassification:
-    """src/model.py:48-60 (fields the training path produces).
+    """src/model.py:48-60 (fields the training path produces, in the reference's order).
 
     ``logits`` is fp32 [B,S,V] and differentiable like the reference's (src/model.py:698,731): it is the
-    compute-dtype (bf16) GEMM output ``logits_bf16`` cast on first access, so a training step that never
-    reads it pays nothing; a loss built on it back-propagates through the fused backward (its gradient is
-    added to the cross-entropy's before the LM-head backward GEMMs)."""
+    compute-dtype (bf16) GEMM output ``logits_bf16`` cast on first access (or the tensor passed as ``logits=``);
+    a loss built on it back-propagates through the fused backward (its gradient is added to the cross-entropy's
+    before the LM-head backward GEMMs)."""
     loss: Optional[torch.Tensor] = None
-    logits_bf16: Optional[torch.Tensor] = None    # [B,S,V] view of the bf16 GEMM output
+    logits: Optional[torch.Tensor] = _LazyLogits()
     emotion_logits: Optional[torch.Tensor] = None
     past_key_values: Optional[tuple] = None
     hidden_states: Optional[tuple] = None
     attentions: Optional[tuple] = None
     cross_attentions: Optional[tuple] = None
+    logits_bf16: Optional[torch.Tensor] = None    # build extra: [B,S,V] view of the bf16 GEMM output
     loss_lm: Optional[torch.Tensor] = None        # build extra: the LM part (PPL = exp(loss_lm))
     loss_emotion: Optional[torch.Tensor] = None   # build extra: the emotion CE part
-    _logits32: Optional[torch.Tensor] = None
-
-    @property
-    def logits(self) -> Optional[torch.Tensor]:
-        if self._logits32 is None and self.logits_bf16 is not None:
-            self._logits32 = self.logits_bf16.float()
-        return self._logits32
 
     def __getitem__(self, i):
         return (self.loss, self.logits, self.emotion_logits)[i]
@@ -242,16 +254,24 @@ class GPT2LMHeadModel(nn.Module):
         # dropout mask stream: seed from torch's default generator (torch.manual_seed makes it reproducible),
         # offset = training forwards so far; under data parallelism rank 0's seed is broadcast so every rank
         # draws the masks one process would draw for the concatenated batch (rows are global)
+        self.reseed_dropout()
+        self.init_weights()
+
+    def reseed_dropout(self) -> None:
+        """Draw the dropout mask stream's seed from torch's default generator and restart its forward count:
+        after ``torch.manual_seed(s)`` the following training forwards draw the same masks as after any other
+        ``torch.manual_seed(s)`` (the reference seeds torch at every ``train()`` start, src/main.py:124,284-289,
+        which fixes its dropout masks).  Under data parallelism rank 0's seed is broadcast (collective)."""
         self._drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        if process_group is not None:
+        pg = self.process_group
+        if pg is not None:
             import torch.distributed as dist
-            if dist.get_world_size(process_group) > 1:
-                bdev = dev if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
+            if dist.get_world_size(pg) > 1:
+                bdev = self.flat.device if dist.get_backend(pg) == "nccl" else torch.device("cpu")
                 t = torch.tensor([self._drop_seed], dtype=torch.int64, device=bdev)
-                dist.broadcast(t, src=dist.get_global_rank(process_group, 0), group=process_group)
+                dist.broadcast(t, src=dist.get_global_rank(pg, 0), group=pg)
                 self._drop_seed = int(t.item())
         self._drop_offset = 0
-        self.init_weights()
 
     # ---- parameters / state_dict ---------------------------------------------------------
     def view(self, name: str, t: Optional[torch.Tensor] = None) -> torch.Tensor:

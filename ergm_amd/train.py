@@ -101,8 +101,20 @@ class Trainer:
         self.model.eval()
         return self._pass(loader, False)
 
-    def train(self, train_loader, valid_loader, num_epochs: int, log=print) -> Tuple[EpochStats, EpochStats]:
-        """src/main.py:125-204: epochs of training + validation, keeping the best-PPL checkpoint."""
+    def train(self, train_loader, valid_loader, num_epochs: int, log=print,
+              seed: Optional[int] = None) -> Tuple[EpochStats, EpochStats]:
+        """src/main.py:125-204: epochs of training + validation, keeping the best-PPL checkpoint.  ``seed``: as the
+        reference's ``fix_seed(args.seed)`` at the start of ``train()`` (src/main.py:124,284-289) — seeds torch,
+        numpy and ``random``, and re-derives the model's dropout mask stream from it, so two runs from the same
+        weights give identical epoch metrics."""
+        if seed is not None:
+            import random
+            import numpy as np
+            random.seed(seed)
+            np.random.seed(seed)
+            torch.manual_seed(seed)
+            if hasattr(self.model, "reseed_dropout"):
+                self.model.reseed_dropout()
         tr = va = None
         start = self.last_epoch + 1
         for epoch in range(start, start + num_epochs):

@@ -495,6 +495,46 @@ def test_grouped_weight_gradient_launches_are_bitwise_the_separate_ones(gpu, mon
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("B,S,E", [(16, 128, 128), (3, 37, 128), (2, 64, 256)])
+def test_fused_optimizer_is_bitwise_the_per_range_update(gpu, B, S, E):
+    """FusedAdamW(fuse=True): every block's Conv1D weights + biases updated in the epilogue of the weight-gradient
+    GEMM that forms their gradient and the LayerNorm parameters in their gradient reduction (the weight-gradient
+    pairs forked after the data-gradient GEMM that last reads the bf16 shadow) give bitwise the parameters, moments,
+    bf16 shadow and losses of the per-range passes over three steps with dropout and a scheduled LR; with
+    keep_grads the gradients too.  B = 16, S = 128 is C2's token count (grouped pipelined launches), B = 3, S = 37
+    an odd token count (register-staged kernels, scalar epilogue)."""
+    from ergm_amd.data import synthetic_batch
+    from ergm_amd.optim import get_polynomial_decay_schedule_with_warmup
+    V = 512
+    runs = []
+    for fuse, keep in ((False, True), (True, True), (True, False)):
+        torch.manual_seed(7)
+        cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64, n_positions=1024)
+        model = GPT2LMHeadModel(cfg, device=gpu)
+        model.load_state_dict(O.init_params(O.OracleConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64,
+                                                           n_positions=1024), seed=71), strict=False)
+        batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=72, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True, fuse=fuse, keep_grads=keep)
+        sched = get_polynomial_decay_schedule_with_warmup(opt, 1, 10, power=2.0)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            out = _run(model, batch, gpu)
+            g = model.flat.grad.clone()
+            opt.step()
+            sched.step()
+            losses.append(out.loss.item())
+        torch.cuda.synchronize()
+        st = opt.state[model.flat]
+        runs.append((model.flat.detach().clone(), model.flat_b16.clone(), st["exp_avg"].clone(),
+                     st["exp_avg_sq"].clone(), losses, g))
+    for r in runs[1:]:
+        for x, y in zip(runs[0][:4], r[:4]):
+            assert torch.equal(x, y)
+        assert runs[0][4] == r[4]
+    assert torch.equal(runs[0][5], runs[1][5])  # keep_grads: the gradients are written too
+
+
 def test_device_train_metrics_match_framework_ops(gpu):
     """GPT2LMHeadModel.set_train_metrics: the loss finalisation accumulates loss, LM loss and emotion argmax
     hits (src/main.py:158-169) exactly as the equivalent torch ops on the step outputs; eval forwards and
