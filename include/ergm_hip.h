@@ -182,7 +182,7 @@ int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols,
 int ergm_quant_weight_fp8(const void* W, int w_dtype, int ldw, int K, int N, void* Wt, int ldt,
                           float* scale, void* amax_ws, void* stream);
 
-/* MX-fp8 (OCP microscaling) GEMM, config 5's forward (and, with ERGM_FP8_BWD, its data-gradient GEMMs): A [M][lda]
+/* MX-fp8 (OCP microscaling) GEMM, config 5's forward: A [M][lda]
  * and B [N][ldb] e4m3fn bytes (k contiguous),
  * each with an e8m0 scale byte per 32-element K block (a_scale [M][ld_sa], b_scale [N][ld_sb]: 2^(byte-127)),
  *   C = epilogue(alpha · Σ_blocks 2^(ea+eb-254) · Σ_{k in block} A[m][k]·B[n][k])
@@ -347,9 +347,12 @@ typedef struct {
                                * (src/model.py:497-498); otherwise a Conv1D projection per modality
                                * (build-side, config 5: 768-d features into a 1024-d backbone) */
     int fp8;                  /* 1: the forward Conv1D GEMMs of every block (and the caption K/V
-                               * GEMM) run on ergm_gemm_f8 with per-row activation / per-column
-                               * weight scales; weights are re-quantised from the bf16 shadow at
-                               * every forward; LM head, backward and optimizer stay bf16/f32 */
+                               * GEMM) run on fp8: ergm_gemm_mx on MX-fp8 operands (default; the
+                               * LayerNorms, the GELU epilogue and the attention forward write the MX
+                               * copies of their outputs) or, with ERGM_FP8_MX=0, ergm_gemm_f8 with
+                               * per-row activation / per-column weight scales; weights are
+                               * re-quantised from the bf16 shadow at every forward; LM head,
+                               * backward and optimizer stay bf16/f32 */
 } ergm_model_dims;
 
 /* Pointer table: names follow the reference state_dict; see ergm_amd/model.py. */

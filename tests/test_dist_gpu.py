@@ -240,6 +240,5 @@ def test_nccl_world1_forced_dp_matches_single_process(gpu, mode):
         for a, b in zip(dp["grads"], ref["grads"]):
             err = ((a - b).norm() / b.norm()).item()
             assert err < 4e-3, err
-        p0 = torch.zeros(0)
         d = ((dp["flat"] - ref["flat"]).norm() / ref["flat"].norm()).item()
         assert d < 1e-3, d

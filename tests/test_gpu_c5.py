@@ -3,12 +3,14 @@ pooled visual / audio features entering through the build-side projection GEMMs 
 reference adds features of width n_embd directly and has no projection; the projection's parity is
 against the oracle restatement, "parity unpinned" by the reference itself).
 
-bf16 gates as in test_gpu_model.py.  The fp8 path (forward Conv1D GEMMs on e4m3 with
-per-row activation / per-column weight scales) is held to SURVEY §8(c)'s fp8 loss gate (rel <= 1e-2)
-and to gates set from its measured deviation (tools/fp8_parity.py on MI355X, medium geometry: loss rel
-6.3e-4, logits max|d| 0.26 of max|logit| 3.3, gradient rel-L2 median 0.056 / max 0.106, against the bf16
-path's 8e-5 / 0.021 / 0.006 / 0.051): logits max-abs <= 0.12 * max|logit|, every gradient rel-L2 <= 0.2.
-The fp8 weights are re-quantised (from the bf16 shadow) at every forward.
+bf16 gates as in test_gpu_model.py.  The fp8 path (forward Conv1D GEMMs on e4m3) runs by default
+on OCP MX-fp8 operands — an e8m0 scale per 32-element K block of every activation row and weight column, consumed by
+the block-scaled MFMA (ergm_gemm_mx); ERGM_FP8_MX=0 selects the per-row activation / per-column weight scales
+(ergm_gemm_f8), which test_fp8_forward_training_step_matches_oracle runs too.  Both are held to SURVEY §8(c)'s fp8
+loss gate (rel <= 1e-2) and to gates set from the measured deviation (tools/fp8_parity.py on MI355X, medium
+geometry, per-row scales: loss rel 6.3e-4, logits max|d| 0.26 of max|logit| 3.3, gradient rel-L2 median 0.056 / max
+0.106, against the bf16 path's 8e-5 / 0.021 / 0.006 / 0.051): logits max-abs <= 0.12 * max|logit|, every gradient
+rel-L2 <= 0.2.  The fp8 weights are re-quantised (from the bf16 shadow) at every forward; the backward is bf16.
 """
 import pytest
 import torch
@@ -83,8 +85,9 @@ def test_gpt2_medium_geometry_with_768d_features(gpu):
 FP8_LOSS_RTOL, FP8_LOGIT_FRAC, FP8_GRAD_RTOL = 1e-2, 0.12, 0.2
 
 
-@pytest.mark.parametrize("geom", ["small", "medium"])
-def test_fp8_forward_training_step_matches_oracle(gpu, geom):
+@pytest.mark.parametrize("geom,mx", [("small", "1"), ("medium", "1"), ("small", "0"), ("medium", "0")])
+def test_fp8_forward_training_step_matches_oracle(gpu, monkeypatch, geom, mx):
+    monkeypatch.setenv("ERGM_FP8_MX", mx)  # read when the model's plan is created
     if geom == "small":
         V, E, Lyr, H, Fd, B, S, kw = 500, 128, 2, 2, 64, 3, 64, dict(vocab_hi=490, sp1=498, sp2=499, eos=489)
     else:

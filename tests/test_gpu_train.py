@@ -122,3 +122,23 @@ def test_trainer_metrics_match_reference_loop(gpu):
     assert abs(va.loss - vw[0]) <= 2e-3 * abs(vw[0]) and abs(va.ppl - vw[1]) <= 2e-2 * abs(vw[1]), (va, vw)
     near_ties = int((z["valid_emotion_margin"] < 2e-2).sum())
     assert abs(va.acc - vw[2]) <= 100.0 * near_ties / 8 + 1e-9, (va, vw, near_ties)
+
+
+def test_train_seed_fixes_dropout_and_metrics(gpu):
+    """Trainer.train(seed=) seeds as the reference's fix_seed at every train() start (src/main.py:124,284-289):
+    two models built under different torch seeds (different dropout mask streams), trained from the same weights
+    with the same seed, give identical epoch metrics and parameters; another seed gives different ones."""
+    from ergm_amd.config import ERGMConfig
+    train_ds, valid_ds = _data(4, 3), _data(2, 4)
+    res = []
+    for build_seed, seed in ((11, 5), (12, 5), (13, 6)):
+        torch.manual_seed(build_seed)
+        cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=2, n_positions=64)  # dropout 0.1
+        model = GPT2LMHeadModel(cfg, device=gpu)
+        model.init_weights(seed=5)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True)
+        tr, va = Trainer(model, opt).train(_loader(train_ds), _loader(valid_ds), 1, log=lambda *_: None, seed=seed)
+        torch.cuda.synchronize()
+        res.append((tr.loss, tr.acc, va.loss, model.flat.detach().clone()))
+    assert res[0][:3] == res[1][:3] and torch.equal(res[0][3], res[1][3])
+    assert res[0][0] != res[2][0]

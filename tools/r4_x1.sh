@@ -13,3 +13,10 @@ BA=--fuse-optim run fuse_noepi$i ERGM_X_EPI=0
 BA=--fuse-optim run fuse_early$i ERGM_X_LATE=0
 BA=--fuse-optim run fuse$i ERGM_NONE=1
 done
+# GPU-only kernel trace of the plain step (the bench's last steps run behind a spin kernel: no host in the loop)
+unset ERGM_LIB_PATH
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/x1_prof -o run --output-format csv -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline > gpurun_out/x1_prof.log 2>&1
+python tools/timeline.py gpurun_out/x1_prof --step -2 --min-us 5 > gpurun_out/x1_timeline.txt 2>&1 || true
+python tools/trace_step.py gpurun_out/x1_prof 40 > gpurun_out/x1_trace_step.txt 2>&1 || true
+rm -f gpurun_out/x1_prof/run_kernel_trace.csv.gz
+head -5 gpurun_out/x1_timeline.txt
