@@ -1,0 +1,10 @@
+#!/bin/bash
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py tests/test_gpu_dropout.py -x -q --timeout 240 --timeout-method thread -k "layernorm or small or c2 or chains or dropout or deterministic" > gpurun_out/ln_tests.log 2>&1 || { tail -40 gpurun_out/ln_tests.log; exit 1; }
+tail -2 gpurun_out/ln_tests.log
+run() { tag=$1; shift; env "$@" timeout -k 10 200 python bench.py --no-cpu-baseline --no-gpu-only > gpurun_out/ln_$tag.json 2> gpurun_out/ln_$tag.err || { tail -20 gpurun_out/ln_$tag.err; exit 1; }; python -c "import json;d=json.loads(open('gpurun_out/ln_$tag.json').read().strip().splitlines()[-1]);print('$tag',d['value'],d['ms_per_step'])"; }
+for i in 1 2 3; do
+run rpw1_$i ERGM_LN_RPW=1
+run rpw2_$i ERGM_LN_RPW=2
+done
