@@ -100,6 +100,13 @@ struct AttnArgs {
     // layout (pitch qpitch rows), row = b·Sq + q; nullptr: none
     uint8_t *qmx, *qms;
     int ldqm, qpitch;
+    // fused short backward (attn_bwd_short_kernel<.., GEMM_DO = true>): dO of head h is formed in the kernel as
+    // dO = gA·Wᵀ over K_g (the residual branch's c_proj data gradient, src/model.py:245 — gA = the branch's output
+    // gradient [B·Sq][lda_g], gW = the c_proj weight [H·64][ldw_g] (Conv1D [in, out], row i = dO column i)) instead of
+    // being read from `dout`
+    const __bf16* gA;
+    const __bf16* gW;
+    int lda_g, ldw_g, K_g;
 };
 
 // Dropout factor of one probability: 1/(1-p) kept, 0 dropped.
@@ -684,8 +691,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 constexpr int AS_MAX = 128;                          // max Sq / Sk of the fused path
 constexpr int AS_TILES = AS_MAX / AT_T;              // 64-row tiles per operand
 constexpr int AS_OPER = AS_TILES * AT_TILE_BYTES;    // 16 KiB per staged operand
-// + the dropout keep bits of the (b, h): [query][AS_TILES] u64
-constexpr int AS_LDS = 4 * AS_OPER + AS_TILES * AS_TILES * AT_TILE_BYTES + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
+// LDS: Q, dO, K staged; the dS tiles [key][query] start at V's staging, which is dead once every wave holds its V
+// fragments (phase 1's first barrier); then LSE, δ and the dropout keep bits of the (b, h) ([query][AS_TILES] u64).
+// 83 KiB: a workgroup fits on a CU beside one 64-KiB GEMM tile of the concurrent weight-gradient stream.
+constexpr int AS_DS = AS_TILES * AS_TILES * AT_TILE_BYTES;  // 32 KiB
+static_assert(AS_DS >= AS_OPER, "dS tiles overlay V's staging");
+constexpr int AS_LDS = 3 * AS_OPER + AS_DS + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
 
 // 128 rows x 64 dims of a token-major operand as two swizzled 64-row tiles (rows >= nrows are zero):
 // the loads are issued first (2 x 16 B per thread), then written to LDS, so several staged operands
@@ -710,15 +721,26 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
     }
 }
 
-template <bool CAUSAL, bool DROP>
+// GEMM_DO: the fused form.  dO [Sq][64] of (b, h) = gA[b·Sq ..][0, K_g) · gW[h·64 ..][0, K_g)ᵀ on the 8 waves (4 x 2
+// grid of 32 x 32, v_mfma_f32_16x16x32_bf16, 64-deep K steps through a 2-stage LDS-DMA ring, the same product order as
+// ergm_gemm, so dO is bitwise the c_proj data-gradient GEMM's bf16 output) while Q, K, V and O are loaded, then
+// rounded to bf16 straight into the staged dO tiles — one launch and one HBM round trip fewer on the backward's
+// critical chain, and dO never goes to memory.  The ring occupies K's staging and the dS region (48 KiB): K and V are
+// held in registers over the GEMM and staged after it, so the fused form needs no more LDS than the plain one.
+constexpr int AS_GA = AS_MAX * GEMM_BK * 2;            // 16 KiB: a 128 x 64 gA stage
+constexpr int AS_GW = AT_D * GEMM_BK * 2;              // 8 KiB: a 64 x 64 gW stage
+constexpr int AS_RING = 2 * (AS_GA + AS_GW);           // 48 KiB
+static_assert(AS_RING <= AS_OPER + AS_DS, "the GEMM ring fits over K's staging and the dS tiles");
+
+template <bool CAUSAL, bool DROP, bool GEMM_DO = false>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sQ = smem;
     char* sdO = sQ + AS_OPER;
     char* sK = sdO + AS_OPER;
     char* sV = sK + AS_OPER;
-    char* sdS = sV + AS_OPER;                          // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
-    float* sL = reinterpret_cast<float*>(sdS + AS_TILES * AS_TILES * AT_TILE_BYTES);
+    char* sdS = sV;                                    // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
+    float* sL = reinterpret_cast<float*>(sdS + AS_DS);
     float* sD = sL + AS_MAX;
     uint64_t* sM = reinterpret_cast<uint64_t*>(sD + AS_MAX);  // dropout keep bits [query][AS_TILES]
     const int b = blockIdx.z, h = blockIdx.y;
@@ -728,7 +750,99 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     const __bf16* dOb = a.dout + (size_t)b * a.Sq * a.lddo + h * AT_D;
     const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
     const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
-    {
+    if constexpr (GEMM_DO) {
+        using TA = GldsTile<AS_MAX, false, 8>;
+        using TW = GldsTile<AT_D, false, 8>;
+        constexpr int LPS = TA::PER_WAVE + TW::PER_WAVE;
+        char* ring = sK;
+        const __bf16* gA = a.gA + (size_t)b * a.Sq * a.lda_g;
+        const int nk = a.K_g / GEMM_BK;
+        auto issue = [&](int kt) {
+            char* st = ring + (kt & 1) * (AS_GA + AS_GW);
+            TA::issue(st, gA, a.lda_g, 0, a.Sq, kt * GEMM_BK, wave);
+            TW::issue(st + AS_GA, a.gW, a.ldw_g, h * AT_D, a.H * AT_D, kt * GEMM_BK, wave);
+        };
+        issue(0);
+        // Q, K, V rows, O for δ and the LSE / keep bits, all in flight beside the GEMM's first stage
+        const Rows128 rq = load_rows(Qb, a.ldq, a.Sq);
+        const Rows128 rk = load_rows(Kb, a.ldk, a.Sk);
+        const Rows128 rv = load_rows(Vb, a.ldv, a.Sk);
+        uint64_t mv = 0;
+        if constexpr (DROP) {
+            const int qq = threadIdx.x / AS_TILES, w = threadIdx.x % AS_TILES;
+            if (qq < a.Sq && w < a.mwords) mv = a.mbits[(((size_t)b * a.H + h) * a.Sq + qq) * a.mwords + w];
+        }
+        const int ql = threadIdx.x >> 2, part = threadIdx.x & 3;
+        bf16x8 y0, y1;
+        float lse = 0.f;
+        if (ql < a.Sq) {
+            const __bf16* od = a.o + ((size_t)b * a.Sq + ql) * a.ldo + h * AT_D + part * 16;
+            y0 = *reinterpret_cast<const bf16x8*>(od);
+            y1 = *reinterpret_cast<const bf16x8*>(od + 8);
+            lse = a.lse[((size_t)b * a.H + h) * a.Sq + ql];
+        }
+        put_rows(sQ, rq);
+        if (DROP && threadIdx.x < AS_MAX * AS_TILES) sM[threadIdx.x] = mv;
+        // dO = gA·gWᵀ: wave (wm, wn) owns rows 32wm.., columns 32wn.. of the 128 x 64 tile
+        const int wm = wave >> 1, wn = wave & 1;
+        FragReader<AS_MAX, false> fa_r;
+        FragReader<AT_D, false> fb_r;
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            wait_stages<LPS, 0>(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kt + 1 < nk) issue(kt + 1);
+            const char* st = ring + (kt & 1) * (AS_GA + AS_GW);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fa[2], fb[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) fa[i] = fa_r.frag(st, wm * 32 + i * 16, ks);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) fb[j] = fb_r.frag(st + AS_GA, wn * 32 + j * 16, ks);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(fa[i], fb[j], acc[i][j]);
+            }
+        }
+        // bf16(dO) into the staged tiles: element (row, col) of the C fragment layout (row 4(l>>4) + r, col l & 15)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = wm * 32 + i * 16 + 4 * g + r, col = wn * 32 + j * 16 + i16;
+                    *reinterpret_cast<__bf16*>(sdO + (row >> 6) * AT_TILE_BYTES + tile_off(row & 63, col >> 3) +
+                                               (col & 7) * 2) = f2bf(acc[i][j][r]);
+                }
+        __syncthreads();  // every wave is done with the ring: K and V take its place
+        put_rows(sK, rk);
+        put_rows(sV, rv);
+        // δ[q] = Σ_d dO·O in the non-fused kernel's order (4 threads per query, 16 dims each)
+        float dsum = 0.f;
+        if (ql < a.Sq) {
+            const char* t = sdO + (ql >> 6) * AT_TILE_BYTES;
+            const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(t + tile_off(ql & 63, part * 2));
+            const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(t + tile_off(ql & 63, part * 2 + 1));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f(x0[j]) * bf2f(y0[j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f(x1[j]) * bf2f(y1[j]);
+        }
+        dsum += __shfl_xor(dsum, 1, 64);
+        dsum += __shfl_xor(dsum, 2, 64);
+        if (part == 0) {
+            sL[ql] = lse;
+            sD[ql] = dsum;
+        }
+    } else {
         const Rows128 rq = load_rows(Qb, a.ldq, a.Sq);
         const Rows128 rdo = load_rows(dOb, a.lddo, a.Sq);
         const Rows128 rk = load_rows(Kb, a.ldk, a.Sk);
@@ -783,6 +897,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         kf[1] = row_frag(sK + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
         vf[0] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 0);
         vf[1] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
+        __syncthreads();  // every wave holds its V fragments: the dS tiles overwrite V's staging
         f32x4 dk[4], dv[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -998,3 +1113,56 @@ extern "C" int ergm_attn_bwd(const void* q, const void* k, const void* v, const 
     else drop ? tiled_bwd<false, true>(gk, gq, s, a) : tiled_bwd<false, false>(gk, gq, s, a);
     return check_launch("attn_bwd");
 }
+
+namespace ergm {
+bool attn_bwd_fusable(int Sq, int Sk, int K) { return Sq <= AS_MAX && Sk <= AS_MAX && !g_attn_generic && K > 0 && K % GEMM_BK == 0; }
+
+// The executor's fused form of "dO = dY·Wᵀ (the c_proj data gradient) ; ergm_attn_bwd(.., dO, ..)" for short
+// sequences (attn_bwd_fusable): attn_bwd_short_kernel<.., GEMM_DO = true>.  Bitwise the two launches' results (the
+// GEMM's product order is ergm_gemm's, δ is summed as in the unfused kernel); no dO or δ is written.
+int attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dy, int lddy, const void* w,
+                   int ldw, int K, const float* lse, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int ldq,
+                   int ldk, int ldv, int ldo, int lddq, int lddk, int lddv, int causal, const ergm_dropout* dropout,
+                   const void* keep_bits, hipStream_t s) {
+    ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, causal));
+    ERGM_CHECK_ARG(attn_bwd_fusable(Sq, Sk, K), "attn_bwd_fused: shape not fusable");
+    ERGM_CHECK_ARG(o && dy && w && lse && dq && dk && dv, "attn_bwd_fused: null argument");
+    ERGM_CHECK_ARG(ldo % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0 && lddy >= K && ldw >= K && lddq % 4 == 0 &&
+                       lddk % 4 == 0 && lddv % 4 == 0,
+                   "attn_bwd_fused: bad leading dims");
+    ERGM_CHECK_ARG(aligned16(o) && aligned16(dy) && aligned16(w), "attn_bwd_fused: O/dY/W must be 16-byte aligned");
+    AttnArgs a{};
+    a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+    a.o = (const __bf16*)o;
+    a.dq = (__bf16*)dq; a.dk = (__bf16*)dk; a.dv = (__bf16*)dv;
+    a.lse = (float*)lse;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+    a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
+    a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
+    a.scale = 0.125f;
+    a.gA = (const __bf16*)dy; a.gW = (const __bf16*)w;
+    a.lda_g = lddy; a.ldw_g = ldw; a.K_g = K;
+    ERGM_TRY(set_drop(a, dropout, const_cast<void*>(keep_bits)));
+    const bool drop = a.mbits != nullptr;
+    static bool attr_set = false;  // benign race: idempotent attribute writes
+    if (!attr_set) {
+        const void* ks[4] = {(const void*)attn_bwd_short_kernel<true, false, true>,
+                             (const void*)attn_bwd_short_kernel<false, false, true>,
+                             (const void*)attn_bwd_short_kernel<true, true, true>,
+                             (const void*)attn_bwd_short_kernel<false, true, true>};
+        for (const void* kf : ks)
+            if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, AS_LDS) != hipSuccess)
+                return fail(ERGM_EHIP, "attn_bwd_fused: cannot raise dynamic LDS limit");
+        attr_set = true;
+    }
+    dim3 grid(1, H, B);
+    if (causal) {
+        if (drop) ERGM_LAUNCH((attn_bwd_short_kernel<true, true, true>), grid, dim3(512), AS_LDS, s, a);
+        else ERGM_LAUNCH((attn_bwd_short_kernel<true, false, true>), grid, dim3(512), AS_LDS, s, a);
+    } else {
+        if (drop) ERGM_LAUNCH((attn_bwd_short_kernel<false, true, true>), grid, dim3(512), AS_LDS, s, a);
+        else ERGM_LAUNCH((attn_bwd_short_kernel<false, false, true>), grid, dim3(512), AS_LDS, s, a);
+    }
+    return check_launch("attn_bwd_fused");
+}
+}  // namespace ergm

@@ -33,6 +33,11 @@ int quant_weights_mx(const MxJobs& J, hipStream_t s);
 int attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk, int ldq,
                 int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits, uint8_t* qmx,
                 uint8_t* qms, int ldqm, int qpitch, hipStream_t s);
+bool attn_bwd_fusable(int Sq, int Sk, int K);
+int attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dy, int lddy, const void* w,
+                   int ldw, int K, const float* lse, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int ldq,
+                   int ldk, int ldv, int ldo, int lddq, int lddk, int lddv, int causal, const ergm_dropout* dropout,
+                   const void* keep_bits, hipStream_t s);
 int quant_rows_mx(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, void* S, int lds,
                   hipStream_t s);
 int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq, float* scale,
@@ -143,6 +148,7 @@ struct ergm_model_plan {
     // the backward's data-gradient chains likewise (bwd_forked: the second chain is running, forked
     // after the head stage and joined by the embedding stage)
     int fwd_chains, bwd_chains;
+    bool attn_fuse;  // attention backward with the c_proj data-gradient GEMM inside (attn_bwd_fused, S <= 128)
     bool dw_group;  // weight-gradient pairs issued behind one side-stream fork run as ONE grouped launch when both
                     // qualify (gemm_dw_pair)
     // stages between a block's backward and its AdamW launch (opt_after_layer): 2 measured best (vs 1: C2 -0.4 %,
@@ -788,6 +794,10 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
     if (const char* e = getenv("ERGM_DW_GROUP")) P->dw_group = atoi(e) != 0;
+    // the c_proj dX GEMM inside the short attention backward: bitwise the two-launch form (ERGM_ATTN_FUSE=0
+    // restores it for the A/B and the parity test)
+    P->attn_fuse = attn_bwd_fusable(d.seq, d.seq, d.n_embd);
+    if (const char* e = getenv("ERGM_ATTN_FUSE")) P->attn_fuse = P->attn_fuse && atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -1374,6 +1384,20 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
+        if (P->attn_fuse) {  // dO = dh2·Wxpᵀ formed inside the attention backward
+            if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
+            if (!P->dry) {
+                const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
+                __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
+                const ergm_dropout dp = attn_drop(P, l, 1, ch.b0[c]);
+                const size_t bhs = (size_t)ch.b0[c] * H * S;
+                ERGM_TRY(attn_bwd_fused(R(a.xq, c, E), kl, kl + E, R(a.xo, c, P->XE), R(dh2, c, E), E,
+                                        LB(P, l, ERGM_T_XPROJ_W), E, E, a.xlse + bhs, R(dxq, c, E), dkl, dkl + E,
+                                        ch.nb[c], H, S, S, E, L2E, L2E, P->XE, E, L2E, L2E, 0, &dp,
+                                        attn_bits(P, l, 1, ch.b0[c]), ch.s[c]));
+            }
+            continue;
+        }
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
         if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
@@ -1401,6 +1425,20 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
+        if (P->attn_fuse) {  // dO = dh1·Wapᵀ formed inside the attention backward
+            if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
+            if (!P->dry) {
+                const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
+                const size_t bhs = (size_t)ch.b0[c] * H * S;
+                const __bf16* q = R(a.qkv, c, 3 * E);
+                __bf16* dq = R(dqkv, c, 3 * E);
+                ERGM_TRY(attn_bwd_fused(q, q + E, q + 2 * E, R(a.ao, c, P->XE), R(dh1, c, E), E,
+                                        LB(P, l, ERGM_T_APROJ_W), E, E, a.lse + bhs, dq, dq + E, dq + 2 * E, ch.nb[c],
+                                        H, S, S, 3 * E, 3 * E, 3 * E, P->XE, 3 * E, 3 * E, 3 * E, 1, &dp,
+                                        attn_bits(P, l, 0, ch.b0[c]), ch.s[c]));
+            }
+            continue;
+        }
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
         if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY

@@ -495,6 +495,32 @@ def test_grouped_weight_gradient_launches_are_bitwise_the_separate_ones(gpu, mon
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("B,S,E,drop", [(16, 128, 128, True), (3, 37, 128, True), (2, 64, 256, False), (1, 2, 128, True),
+                                         (2, 100, 128, False)])
+def test_fused_attention_backward_is_bitwise_the_two_launches(gpu, monkeypatch, B, S, E, drop):
+    """The c_proj data-gradient GEMM formed inside the short attention backward (attn_bwd_fused, one workgroup per
+    (sample, head), dO staged in LDS only) gives bitwise the loss and every gradient of the GEMM + attention
+    backward launches (ERGM_ATTN_FUSE=0), self (causal) and cross attention, with and without dropout; ragged
+    sequence lengths (37, 100: a partial second 64-row tile) and S = 2."""
+    from ergm_amd.data import synthetic_batch
+    V = 512
+    res = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("ERGM_ATTN_FUSE", fuse)
+        torch.manual_seed(9)
+        kw = {} if drop else NO_DROPOUT
+        cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64, n_positions=1024, **kw)
+        model = GPT2LMHeadModel(cfg, device=gpu)
+        model.load_state_dict(O.init_params(O.OracleConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64,
+                                                           n_positions=1024), seed=81), strict=False)
+        batch = synthetic_batch(B, S, n_turns=2 if S < 8 else 3, feat_dim=E, seed=82, vocab_hi=V - 3, sp1=V - 2,
+                                sp2=V - 1, eos=V - 4)
+        out = _run(model, batch, gpu)
+        res.append((out.loss.detach().clone(), model.flat.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("B,S,E", [(16, 128, 128), (3, 37, 128), (2, 64, 256)])
 def test_fused_optimizer_is_bitwise_the_per_range_update(gpu, B, S, E):
     """FusedAdamW(fuse=True): every block's Conv1D weights + biases updated in the epilogue of the weight-gradient
