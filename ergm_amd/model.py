@@ -159,6 +159,8 @@ def _train_step_setup(ctx, inputs, output):
     model = _MODELS.get(handle)
     ctx.fwd_id = model._runners[tuple(key)].fwd_count if model is not None and not _compiling(output[0]) else -1
     ctx.mark_non_differentiable(output[2])
+    if model is not None and _compiling(output[0]) and not model.compiled_logits_grad:
+        ctx.mark_non_differentiable(output[1])
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(inputs[0])
 
@@ -226,6 +228,11 @@ torch.library.register_autograd("ergm::train_step", _train_step_grad, setup_cont
 
 class GPT2LMHeadModel(nn.Module):
     num_emotions = NUM_EMOTIONS
+    # Under torch.compile AOTAutograd hands every differentiable output a tangent — zeros for logits the loss
+    # ignores — and the backward would then add a T x vocab bf16 zero gradient into dlogits (~200 MB of traffic at
+    # C2).  The compiled step therefore returns non-differentiable logits unless this is set; eager mode keeps them
+    # differentiable either way (no tangent is materialised there).
+    compiled_logits_grad = False
 
     def __init__(self, config, device=None, process_group=None):
         super().__init__()

@@ -608,11 +608,36 @@ def test_custom_op_registration_and_torch_compile(gpu):
         out = fn(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
                  emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
                  auds=kw["audio_feat"])
+        # compiled: the logits come back non-differentiable (no zero tangent pushed through dlogits) unless the
+        # model opts in with compiled_logits_grad
+        assert out.logits.requires_grad == (not compiled)
         out.loss.backward()
         torch.cuda.synchronize()
-        outs.append((out.loss.detach().clone(), out.logits.clone(), model.flat.grad.clone()))
+        outs.append((out.loss.detach().clone(), out.logits.detach().clone(), model.flat.grad.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_compiled_logits_gradient_opt_in(gpu):
+    """GPT2LMHeadModel.compiled_logits_grad = True: under torch.compile a loss on the logits reaches the parameters
+    as in eager mode (the same dlogits contribution through the native backward)."""
+    rec = _load("tiny_e64.npz")
+    grads = []
+    for compiled in (False, True):
+        _, _, _, model, batch = _setup(rec, gpu)
+        model.compiled_logits_grad = True
+        kw = {k: v.to(gpu) for k, v in batch.items()}
+        fn = torch.compile(model) if compiled else model
+        model.flat.grad = None
+        out = fn(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
+                 emotion_labels=kw["emotion_labels"], caption_ids=kw["caption_ids"], imgs=kw["visual_feat"],
+                 auds=kw["audio_feat"])
+        assert out.logits.requires_grad
+        (out.loss + 1e-3 * out.logits.float().square().mean()).backward()
+        torch.cuda.synchronize()
+        grads.append(model.flat.grad.clone())
+    # inductor may order the square-mean's gradient differently from eager: a bf16 rounding of dlogits apart
+    assert ((grads[0] - grads[1]).norm() / grads[0].norm()).item() <= 1e-3
 
 
 def test_logits_are_fp32_and_differentiable(gpu):
