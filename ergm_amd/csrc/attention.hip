@@ -107,6 +107,10 @@ struct AttnArgs {
     const __bf16* gA;
     const __bf16* gW;
     int lda_g, ldw_g, K_g;
+    // fused cross-attention forward (attn_fwd_qgemm_kernel): Q of head h formed in the kernel as
+    // bf16(gA·gW + gbias) over K_g (the query projection, src/model.py:311-329: gA = LN_x output [B·Sq][lda_g],
+    // gW = the Conv1D weight [K_g][ldw_g], column h·64 + d), also stored to `q` for the backward
+    const float* gbias;
 };
 
 // Dropout factor of one probability: 1/(1-p) kept, 0 dropped.
@@ -496,6 +500,115 @@ __global__ __launch_bounds__(256, DROP ? 3 : 4) void attn_fwd_kernel(AttnArgs a)
         const char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
         fwd_tile<CAUSAL, DROP>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l, a.drop,
                                arow, mrow ? mrow + kt : nullptr);
+    }
+    fwd_store(a, b, h, q, o, m, l);
+}
+
+// Cross-attention forward with the query projection inside (non-causal): the workgroup of (query block, h, b)
+// first forms its 64 x 64 Q tile = bf16(LN_x rows · Wq[:, h·64 ..] + bias) on its 4 waves (2 x 2 grid of 32 x 32,
+// 64-deep K steps through a 3-stage LDS-DMA ring: the product order of the GEMM's 64x64 configuration, so Q is
+// bitwise the q GEMM's output), stores it (the backward's operand) and stages it in LDS for the Q fragments, then
+// runs attn_fwd_kernel's key loop over the same ring.  One launch and one Q round trip fewer per block and chain on
+// the forward, which is latency-bound (profiles/r04_experiments.txt #10).
+constexpr int QG_STAGES = 3;
+constexpr int QG_STAGE = 2 * AT_TILE_BYTES;  // A 64 x 64 + W 64 x 64 (bf16)
+
+template <int NS, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_qgemm_kernel(AttnArgs a) {
+    constexpr int RING = QG_STAGES * QG_STAGE > NS * 2 * AT_TILE_BYTES ? QG_STAGES * QG_STAGE : NS * 2 * AT_TILE_BYTES;
+    __shared__ __attribute__((aligned(16))) char ring[RING];
+    __shared__ __attribute__((aligned(16))) char sQ[AT_TILE_BYTES];
+    const AttnBlock blk = attn_block();
+    const int b = blk.b, h = blk.h;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int i16 = lane & 15, g = lane >> 4;
+    const int qblk = blk.x * AT_T;
+    const int q = qblk + wave * 16 + i16;  // this lane's query
+    const float c = a.scale * AT_LOG2E;
+    {
+        using TA = GldsTile<AT_T, false, 4>;  // LN_x rows, k contiguous
+        using TW = GldsTile<AT_D, true, 4>;   // Wq [k][n]: n contiguous
+        constexpr int LPS = TA::PER_WAVE + TW::PER_WAVE;
+        const __bf16* gA = a.gA + (size_t)b * a.Sq * a.lda_g;
+        const int nk = a.K_g / GEMM_BK;
+        auto issue = [&](int kt) {
+            char* st = ring + (kt % QG_STAGES) * QG_STAGE;
+            TA::issue(st, gA, a.lda_g, qblk, a.Sq, kt * GEMM_BK, wave);
+            TW::issue(st + AT_TILE_BYTES, a.gW, a.ldw_g, h * AT_D, a.H * AT_D, kt * GEMM_BK, wave);
+        };
+        for (int s = 0; s < QG_STAGES - 1 && s < nk; ++s) issue(s);
+        const int wm = wave >> 1, wn = wave & 1;
+        FragReader<AT_T, false> fa_r;
+        FragReader<AT_D, true> fb_r;
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            wait_stages<LPS, QG_STAGES - 2>(min(QG_STAGES - 2, nk - 1 - kt));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kt + QG_STAGES - 1 < nk) issue(kt + QG_STAGES - 1);
+            const char* st = ring + (kt % QG_STAGES) * QG_STAGE;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 fa[2], fb[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) fa[i] = fa_r.frag(st, wm * 32 + i * 16, ks);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) fb[j] = fb_r.frag(st + AT_TILE_BYTES, wn * 32 + j * 16, ks);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(fa[i], fb[j], acc[i][j]);
+            }
+        }
+        // Q = bf16(acc + bias) (the GEMM's EPI_BIAS arithmetic): to the global q (rows < Sq) and the LDS tile
+        // (rows >= Sq zero, as attn_fwd_kernel loads them)
+        __bf16* Qg = const_cast<__bf16*>(a.q) + ((size_t)b * a.Sq + qblk) * a.ldq + h * AT_D;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = wn * 32 + j * 16 + i16;
+                const float bias = a.gbias[h * AT_D + col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = wm * 32 + i * 16 + 4 * g + r;
+                    const bool live = qblk + row < a.Sq;
+                    const __bf16 v = f2bf(acc[i][j][r] + bias);
+                    if (live) Qg[(size_t)row * a.ldq + col] = v;
+                    *reinterpret_cast<__bf16*>(sQ + tile_off(row, col >> 3) + (col & 7) * 2) = live ? v : f2bf(0.f);
+                }
+            }
+        __syncthreads();  // Q staged; every wave is done with the GEMM's ring
+    }
+    bf16x8 qf[2];
+    qf[0] = row_frag(sQ, wave * 16, 0);
+    qf[1] = row_frag(sQ, wave * 16, 1);
+
+    const __bf16* Kb = a.k + (size_t)b * a.Sk * a.ldk + h * AT_D;
+    const __bf16* Vb = a.v + (size_t)b * a.Sk * a.ldv + h * AT_D;
+    f32x4 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    const int nkt = (a.Sk + AT_T - 1) / AT_T;
+    auto issue = [&](int kt) {
+        char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
+        AttnTile::issue(st, Kb, a.ldk, kt * AT_T, a.Sk, 0, wave);
+        AttnTile::issue(st + AT_TILE_BYTES, Vb, a.ldv, kt * AT_T, a.Sk, 0, wave);
+    };
+    const int64_t arow = ((int64_t)b * a.H + h) * a.Sq + q;  // dropout row of this lane's query
+    uint64_t* mrow = DROP && q < a.Sq ? a.mbits + arow * a.mwords : nullptr;
+    for (int s = 0; s < NS - 1 && s < nkt; ++s) issue(s);
+    for (int kt = 0; kt < nkt; ++kt) {
+        ring_sync<4, NS>(min(NS - 2, nkt - 1 - kt));
+        if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+        const char* st = ring + (kt % NS) * 2 * AT_TILE_BYTES;
+        fwd_tile<false, DROP>(st, st + AT_TILE_BYTES, kt * AT_T, q, qblk + wave * 16, a.Sk, c, qf, o, m, l, a.drop, arow,
+                              mrow ? mrow + kt : nullptr);
     }
     fwd_store(a, b, h, q, o, m, l);
 }
@@ -1164,5 +1277,33 @@ int attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, c
         else ERGM_LAUNCH((attn_bwd_short_kernel<false, false, true>), grid, dim3(512), AS_LDS, s, a);
     }
     return check_launch("attn_bwd_fused");
+}
+}  // namespace ergm
+
+namespace ergm {
+// The executor's fused form of "q = LN_x·Wq + bq ; ergm_attn_fwd(q, K, V, ..., causal = 0)" (attn_fwd_qgemm_kernel):
+// bitwise the two launches' q, O, LSE and keep bits.
+int attn_fwd_qgemm(const void* x, int ldx, const void* w, int ldw, const float* bias, int K, void* q, int ldq,
+                   const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk, int ldk, int ldv,
+                   int ldo, const ergm_dropout* dropout, void* keep_bits, hipStream_t s) {
+    ERGM_TRY(check_common(q, k, v, B, H, Sq, Sk, ldq, ldk, ldv, 0));
+    ERGM_CHECK_ARG(x && w && bias && o && lse, "attn_fwd_qgemm: null argument");
+    ERGM_CHECK_ARG(K > 0 && K % GEMM_BK == 0 && ldx % 8 == 0 && ldx >= K && ldw % 8 == 0 && ldw >= H * AT_D,
+                   "attn_fwd_qgemm: bad K / leading dims");
+    ERGM_CHECK_ARG(aligned16(x) && aligned16(w), "attn_fwd_qgemm: x / w must be 16-byte aligned");
+    ERGM_CHECK_ARG(ldo % 4 == 0 && ldo >= H * AT_D, "attn_fwd_qgemm: bad output");
+    AttnArgs a{};
+    a.q = (const __bf16*)q; a.k = (const __bf16*)k; a.v = (const __bf16*)v;
+    a.out = (__bf16*)o; a.lse = lse;
+    a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+    a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
+    a.scale = 0.125f;
+    a.gA = (const __bf16*)x; a.gW = (const __bf16*)w; a.gbias = bias;
+    a.lda_g = ldx; a.ldw_g = ldw; a.K_g = K;
+    ERGM_TRY(set_drop(a, dropout, keep_bits));
+    dim3 grid(cdiv(Sq, AT_T), H, B);
+    if (a.mbits) ERGM_LAUNCH((attn_fwd_qgemm_kernel<2, true>), grid, dim3(256), 0, s, a);
+    else ERGM_LAUNCH((attn_fwd_qgemm_kernel<2, false>), grid, dim3(256), 0, s, a);
+    return check_launch("attn_fwd_qgemm");
 }
 }  // namespace ergm

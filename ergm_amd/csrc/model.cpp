@@ -34,6 +34,9 @@ int attn_fwd_mx(const void* q, const void* k, const void* v, void* o, float* lse
                 int ldk, int ldv, int ldo, int causal, const ergm_dropout* dropout, void* keep_bits, uint8_t* qmx,
                 uint8_t* qms, int ldqm, int qpitch, hipStream_t s);
 bool attn_bwd_fusable(int Sq, int Sk, int K);
+int attn_fwd_qgemm(const void* x, int ldx, const void* w, int ldw, const float* bias, int K, void* q, int ldq,
+                   const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk, int ldk, int ldv,
+                   int ldo, const ergm_dropout* dropout, void* keep_bits, hipStream_t s);
 int attn_bwd_fused(const void* q, const void* k, const void* v, const void* o, const void* dy, int lddy, const void* w,
                    int ldw, int K, const float* lse, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int ldq,
                    int ldk, int ldv, int ldo, int lddq, int lddk, int lddv, int causal, const ergm_dropout* dropout,
@@ -149,6 +152,7 @@ struct ergm_model_plan {
     // after the head stage and joined by the embedding stage)
     int fwd_chains, bwd_chains;
     bool attn_fuse;  // attention backward with the c_proj data-gradient GEMM inside (attn_bwd_fused, S <= 128)
+    bool xq_fuse;    // cross-attention forward with the query projection inside (attn_fwd_qgemm; bf16 forward)
     bool dw_group;  // weight-gradient pairs issued behind one side-stream fork run as ONE grouped launch when both
                     // qualify (gemm_dw_pair)
     // stages between a block's backward and its AdamW launch (opt_after_layer): 2 measured best (vs 1: C2 -0.4 %,
@@ -798,6 +802,9 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     // restores it for the A/B and the parity test)
     P->attn_fuse = attn_bwd_fusable(d.seq, d.seq, d.n_embd);
     if (const char* e = getenv("ERGM_ATTN_FUSE")) P->attn_fuse = P->attn_fuse && atoi(e) != 0;
+    // the query projection inside the cross-attention forward (bf16 forward only; ERGM_XQ_FUSE=0: two launches)
+    P->xq_fuse = !P->f8 && d.n_embd % 64 == 0;
+    if (const char* e = getenv("ERGM_XQ_FUSE")) P->xq_fuse = P->xq_fuse && atoi(e) != 0;
     P->bwd_forked = false;
     P->per_stage_join = true;
     P->fwd2 = nullptr;
@@ -1068,7 +1075,7 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     if (on(4) && !P->dry)
         ERGM_TRY(layernorm_fwd_ld(x1, LF(P, l, ERGM_T_LNX_W), LF(P, l, ERGM_T_LNX_B), a.lnx, P->XE, a.mx, a.rx, T, E,
                                   d.eps, s, qa, E, lsa, lxa, P->T));
-    if (on(5)) {
+    if (on(5) && !P->xq_fuse) {
         if (f8)
             ERGM_TRY(gemm8(P, s, T, E, E, qa, sa, xa, w8 ? w8->w[2] : nullptr, w8 ? w8->sc[2] : nullptr,
                            w8 ? w8->sx[2] : nullptr, a.xq, E, ERGM_BF16, ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
@@ -1078,9 +1085,15 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
     }
     const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
     if (on(6) && l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
-    if (on(6) && !P->dry)
-        ERGM_TRY(attn_fwd_mx(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
-                             attn_bits(P, l, 1, b0), amx ? qa : nullptr, amx ? xa : nullptr, E, P->T, s));
+    if (on(6) && !P->dry) {
+        if (P->xq_fuse)  // q = LN_x·Wq + bq formed inside the cross-attention forward
+            ERGM_TRY(attn_fwd_qgemm(a.lnx, P->XE, LB(P, l, ERGM_T_XQ_W), E, LF(P, l, ERGM_T_XQ_B), E, a.xq, E, kl,
+                                    kl + E, a.xo, a.xlse, nb, H, S, S, L2E, L2E, P->XE, &dp_cross,
+                                    attn_bits(P, l, 1, b0), s));
+        else
+            ERGM_TRY(attn_fwd_mx(a.xq, kl, kl + E, a.xo, a.xlse, nb, H, S, S, E, L2E, L2E, P->XE, 0, &dp_cross,
+                                 attn_bits(P, l, 1, b0), amx ? qa : nullptr, amx ? xa : nullptr, E, P->T, s));
+    }
     if (on(7)) {
         if (f8) {
             if (!P->dry && !amx) ERGM_TRY(quant_act(P, a.xo, P->XE, T, E, qa, sa, xa, s));

@@ -521,6 +521,31 @@ def test_fused_attention_backward_is_bitwise_the_two_launches(gpu, monkeypatch, 
     assert torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("B,S,E,drop", [(16, 128, 128, True), (3, 37, 128, True), (2, 64, 256, False), (1, 2, 128, True),
+                                         (2, 200, 128, True)])
+def test_fused_cross_attention_forward_is_bitwise_the_two_launches(gpu, monkeypatch, B, S, E, drop):
+    """The query projection formed inside the cross-attention forward (attn_fwd_qgemm, Q staged in LDS and stored
+    for the backward) gives bitwise the loss, logits and every gradient of the q GEMM + attention launches
+    (ERGM_XQ_FUSE=0), with and without attention dropout; ragged and multi-tile lengths (37, 200) and S = 2."""
+    from ergm_amd.data import synthetic_batch
+    V = 512
+    res = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("ERGM_XQ_FUSE", fuse)
+        torch.manual_seed(11)
+        kw = {} if drop else NO_DROPOUT
+        cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64, n_positions=1024, **kw)
+        model = GPT2LMHeadModel(cfg, device=gpu)
+        model.load_state_dict(O.init_params(O.OracleConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64,
+                                                           n_positions=1024), seed=91), strict=False)
+        batch = synthetic_batch(B, S, n_turns=2 if S < 8 else 3, feat_dim=E, seed=92, vocab_hi=V - 3, sp1=V - 2,
+                                sp2=V - 1, eos=V - 4)
+        out = _run(model, batch, gpu)
+        res.append((out.loss.detach().clone(), out.logits_bf16.clone(), model.flat.grad.clone()))
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("B,S,E", [(16, 128, 128), (3, 37, 128), (2, 64, 256)])
 def test_fused_optimizer_is_bitwise_the_per_range_update(gpu, B, S, E):
     """FusedAdamW(fuse=True): every block's Conv1D weights + biases updated in the epilogue of the weight-gradient
