@@ -22,6 +22,11 @@
 
 namespace ergm {
 
+// Internal epilogue code of the AdamW weight-gradient epilogue (ergm_gemm_desc::adamw): its own kernel instantiations,
+// so the parameter / moment registers of the update never weigh on the ordinary epilogues (a runtime branch in every
+// f32 epilogue raised their VGPR counts by up to 2x and cost C5 2-4 %, profiles/r04_experiments.txt #12).
+constexpr int EPI_ADAMW = 64;
+
 
 struct GemmArgs {
     const __bf16* A;
@@ -126,11 +131,9 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
         v *= bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);  // stored gelu'(pre)
     }
     size_t idx = (size_t)m * a.ldc + n;
-    if constexpr (EPI == ERGM_EPI_NONE && !OUT_BF16) {
-        if (a.opt.p) {
-            adam_store1(a.opt, reinterpret_cast<float*>(a.C), idx, v);
-            return;
-        }
+    if constexpr (EPI == EPI_ADAMW) {
+        adam_store1(a.opt, reinterpret_cast<float*>(a.C), idx, v);
+        return;
     }
     if (OUT_BF16) {
         reinterpret_cast<__bf16*>(a.C)[idx] = f2bf(v);
@@ -177,11 +180,9 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
         for (int j = 0; j < 8; ++j) v[j] *= bf2f(x[j]);
     }
     const size_t idx = (size_t)m * a.ldc + n;
-    if constexpr (EPI == ERGM_EPI_NONE && !OUT_BF16) {
-        if (a.opt.p) {
-            adam_store8(a.opt, reinterpret_cast<float*>(a.C), idx, v);
-            return;
-        }
+    if constexpr (EPI == EPI_ADAMW) {
+        adam_store8(a.opt, reinterpret_cast<float*>(a.C), idx, v);
+        return;
     }
     if (OUT_BF16) {
         bf16x8 o;
@@ -240,8 +241,8 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
                         t[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
         }
         __syncthreads();
-        if constexpr (EPI == ERGM_EPI_NONE && !OUT_BF16 && !RS && !QMX) {
-            if (a.opt.p && !slab) {  // AdamW epilogue: every parameter / moment load of the pass in flight at once
+        if constexpr (EPI == EPI_ADAMW && !OUT_BF16 && !RS && !QMX) {
+            if (!slab) {  // AdamW epilogue: every parameter / moment load of the pass in flight at once
                 constexpr int CPT = (WM * CPR + NT - 1) / NT;
                 f32x4 pv[CPT][2], mv[CPT][2], vv[CPT][2];
                 bool ok[CPT];
@@ -730,13 +731,13 @@ struct GemmArgs2 {
     GemmArgs a[2];
     int b1;
 };
-template <int BM, int BN, int WGM, int WGN, int NS, int IL = 0>
+template <int BM, int BN, int WGM, int WGN, int NS, int IL = 0, int EPI = ERGM_EPI_NONE>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_dw2_kernel(GemmArgs2 g) {
     const int b = blockIdx.x;
     const int pr = b < g.b1 ? 0 : 1;
     const int bb = pr == 0 ? b : b - g.b1;
     if (pr == 0 && b >= g.a[0].tiles_m * g.a[0].tiles_n) return;
-    gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, ERGM_EPI_NONE, false, false, IL>(g.a[pr], bb);
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, EPI, false, false, IL>(g.a[pr], bb);
 }
 
 // Warp-specialised variant: NP producer waves only issue the LDS-DMA fills, the WGM x WGN consumer
@@ -1130,7 +1131,7 @@ static constexpr bool combo_ok(bool akm, bool bkn, int e, bool ob) {
     return (!akm && bkn && (e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) && ob) ||
            (!akm && bkn && e == ERGM_EPI_BIAS_RESID && !ob) || (!akm && bkn && e == ERGM_EPI_NONE && !ob) ||
            (!akm && !bkn && e == ERGM_EPI_NONE) || (!akm && !bkn && e == ERGM_EPI_GELU_BWD && ob) ||
-           (akm && bkn && e == ERGM_EPI_NONE && !ob);
+           (akm && bkn && (e == ERGM_EPI_NONE || e == EPI_ADAMW) && !ob);
 }
 
 static bool pipe_ok(const ergm_gemm_desc* d) {
@@ -1385,6 +1386,10 @@ static void launch_any(const GemmArgs& a, const GemmPlan& p, hipStream_t s) {
 
 template <int EPI, bool OB>
 static void launch_layout(const GemmArgs& a, const GemmPlan& p, int al, int bl, hipStream_t s) {
+    if constexpr (EPI == EPI_ADAMW) {  // validate_desc: weight-gradient layout only
+        launch_any<true, true, EPI, OB>(a, p, s);
+        return;
+    }
     if (al == ERGM_MK && bl == ERGM_NK) launch_any<false, false, EPI, OB>(a, p, s);
     else if (al == ERGM_MK && bl == ERGM_KN) launch_any<false, true, EPI, OB>(a, p, s);
     else if (al == ERGM_KM && bl == ERGM_NK) launch_any<true, false, EPI, OB>(a, p, s);
@@ -1762,6 +1767,11 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
             else launch_reduce<E, false>(a, p.split, s);                   \
         }                                                                 \
         break;
+    if (d->adamw) {  // the AdamW epilogue: its own instantiations (validate_desc: KM x KN, f32 C)
+        launch_layout<EPI_ADAMW, false>(a, p, d->a_layout, d->b_layout, s);
+        if (p.split > 1) launch_reduce<EPI_ADAMW, false>(a, p.split, s);
+        return check_launch("ergm_gemm");
+    }
     switch (e) {
         ERGM_EPI_CASE(ERGM_EPI_NONE)
         ERGM_EPI_CASE(ERGM_EPI_BIAS)
@@ -1778,12 +1788,12 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
 }
 
 namespace ergm {
-template <int C>
+template <int C, int EPI = ERGM_EPI_NONE>
 static void launch_dw2_cfg(const GemmArgs2& g, int nblocks, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
     static_assert(c.np == 0 && !c.direct, "grouped dW launch: pipelined kernels with the staged epilogue only");
     constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
-    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il>;
+    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il, EPI>;
     static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
     (void)attr;
     ERGM_LAUNCH(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
@@ -1800,6 +1810,7 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
             d[i]->c_dtype != ERGM_F32 || d[i]->split_k > 1 || !pipe_ok(d[i]))
             return ERGM_EUNSUPPORTED;
     }
+    if ((d[0]->adamw == nullptr) != (d[1]->adamw == nullptr)) return ERGM_EUNSUPPORTED;  // one epilogue per launch
     GemmPlan p[2] = {plan_gemm(d[0]), plan_gemm(d[1])};
     const int cfg = p[0].cfg;
     if (cfg < 0 || (cfg >= 16 && kCfgs[cfg].il == 0) || kCfgs[cfg].ks != 1 || p[1].cfg != cfg || p[0].split != 1 ||
@@ -1819,6 +1830,13 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
     g.b1 = (n0 + 7) & ~7;
     const int nb = g.b1 + n1;
     hipStream_t s = as_stream(stream);
+    if (d[0]->adamw) {  // AdamW epilogue pairs: the configurations the executor's block pairs plan to
+        if (cfg == 0) launch_dw2_cfg<0, EPI_ADAMW>(g, nb, s);
+        else if (cfg == 2) launch_dw2_cfg<2, EPI_ADAMW>(g, nb, s);
+        else if (cfg == 10) launch_dw2_cfg<10, EPI_ADAMW>(g, nb, s);
+        else return ERGM_EUNSUPPORTED;
+        return check_launch("gemm_dw_pair");
+    }
     switch (cfg) {
         case 0: launch_dw2_cfg<0>(g, nb, s); break;
         case 1: launch_dw2_cfg<1>(g, nb, s); break;

@@ -1345,6 +1345,11 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     return ln_bwd(P, s, P->resid[3 * L], P->mf, P->rf, p.ln_f_w, p.g_ln_f_w, p.g_ln_f_b, P->dhb[3 * L], 3 * L);
 }
 
+// The fused attention backward (dO GEMM inside) runs one 512-thread workgroup per (sample, head); with more of them
+// than the chip has CUs its GEMM part runs in rounds and the form loses to the two launches (C5, B·H = 512: -2.5 %;
+// C2, 192: level, profiles/r04_experiments.txt #12).
+constexpr int kAttnFuseMaxWg = 256;
+
 int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     const int E = d.n_embd, F = d.n_inner, H = d.n_head, S = d.seq, L2E = P->L2E;
@@ -1397,7 +1402,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
-        if (P->attn_fuse) {  // dO = dh2·Wxpᵀ formed inside the attention backward
+        if (P->attn_fuse && ch.nb[c] * H <= kAttnFuseMaxWg) {  // dO = dh2·Wxpᵀ formed inside the attention backward
             if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
             if (!P->dry) {
                 const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1438,7 +1443,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
     ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), true));
     for (int c = 0; c < ch.n; ++c) {
-        if (P->attn_fuse) {  // dO = dh1·Wapᵀ formed inside the attention backward
+        if (P->attn_fuse && ch.nb[c] * H <= kAttnFuseMaxWg) {  // dO = dh1·Wapᵀ formed inside the attention backward
             if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
             if (!P->dry) {
                 const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
