@@ -804,12 +804,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 constexpr int AS_MAX = 128;                          // max Sq / Sk of the fused path
 constexpr int AS_TILES = AS_MAX / AT_T;              // 64-row tiles per operand
 constexpr int AS_OPER = AS_TILES * AT_TILE_BYTES;    // 16 KiB per staged operand
-// LDS: Q, dO, K staged; the dS tiles [key][query] start at V's staging, which is dead once every wave holds its V
-// fragments (phase 1's first barrier); then LSE, δ and the dropout keep bits of the (b, h) ([query][AS_TILES] u64).
-// 83 KiB: a workgroup fits on a CU beside one 64-KiB GEMM tile of the concurrent weight-gradient stream.
+// LDS: Q, dO, K, V staged, the dS tiles [key][query], then LSE, δ and the dropout keep bits of the (b, h)
+// ([query][AS_TILES] u64): 99 KiB.  (Placing the dS tiles over V's staging — dead once every wave holds its V
+// fragments — brings it to 83 KiB, room beside one 64-KiB GEMM tile of the concurrent weight-gradient stream; the
+// co-residency measured level at C2 and -1.5 % at C5, profiles/r04_experiments.txt #13.)
 constexpr int AS_DS = AS_TILES * AS_TILES * AT_TILE_BYTES;  // 32 KiB
-static_assert(AS_DS >= AS_OPER, "dS tiles overlay V's staging");
-constexpr int AS_LDS = 3 * AS_OPER + AS_DS + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
+constexpr int AS_LDS = 4 * AS_OPER + AS_DS + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
 
 // 128 rows x 64 dims of a token-major operand as two swizzled 64-row tiles (rows >= nrows are zero):
 // the loads are issued first (2 x 16 B per thread), then written to LDS, so several staged operands
@@ -838,12 +838,13 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
 // grid of 32 x 32, v_mfma_f32_16x16x32_bf16, 64-deep K steps through a 2-stage LDS-DMA ring, the same product order as
 // ergm_gemm, so dO is bitwise the c_proj data-gradient GEMM's bf16 output) while Q, K, V and O are loaded, then
 // rounded to bf16 straight into the staged dO tiles — one launch and one HBM round trip fewer on the backward's
-// critical chain, and dO never goes to memory.  The ring occupies K's staging and the dS region (48 KiB): K and V are
-// held in registers over the GEMM and staged after it, so the fused form needs no more LDS than the plain one.
+// critical chain, and dO never goes to memory.  The ring occupies K's and V's staging and half of the dS region
+// (48 KiB): K and V are held in registers over the GEMM and staged after it, so the fused form needs no more LDS
+// than the plain one.
 constexpr int AS_GA = AS_MAX * GEMM_BK * 2;            // 16 KiB: a 128 x 64 gA stage
 constexpr int AS_GW = AT_D * GEMM_BK * 2;              // 8 KiB: a 64 x 64 gW stage
 constexpr int AS_RING = 2 * (AS_GA + AS_GW);           // 48 KiB
-static_assert(AS_RING <= AS_OPER + AS_DS, "the GEMM ring fits over K's staging and the dS tiles");
+static_assert(AS_RING <= 2 * AS_OPER + AS_DS, "the GEMM ring fits over K's and V's staging and the dS tiles");
 
 template <bool CAUSAL, bool DROP, bool GEMM_DO = false>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     char* sdO = sQ + AS_OPER;
     char* sK = sdO + AS_OPER;
     char* sV = sK + AS_OPER;
-    char* sdS = sV;                                    // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
+    char* sdS = sV + AS_OPER;                          // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
     float* sL = reinterpret_cast<float*>(sdS + AS_DS);
     float* sD = sL + AS_MAX;
     uint64_t* sM = reinterpret_cast<uint64_t*>(sD + AS_MAX);  // dropout keep bits [query][AS_TILES]
@@ -1010,7 +1011,6 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         kf[1] = row_frag(sK + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
         vf[0] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 0);
         vf[1] = row_frag(sV + kt * AT_TILE_BYTES, (wave & 3) * 16, 1);
-        __syncthreads();  // every wave holds its V fragments: the dS tiles overwrite V's staging
         f32x4 dk[4], dv[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
