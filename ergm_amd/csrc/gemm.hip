@@ -1239,15 +1239,9 @@ static GemmPlan plan_gemm(const ergm_gemm_desc* d) {
             // us in-step, profiles/r01_lmhead_probe.txt; c6s5 at C4, c6s4 at C5)
             p.cfg = 6;
             split = (int)std::max(1L, std::min(16L, 256 / std::max(1L, tiles_of(M, N, 256, 256))));
-            // opt-in (ERGM_XCD_SPLIT=1), at most 32 tiles (one XCD's CUs): 8 K slices, one per XCD, so each slice
-            // of both operands is fetched into one L2 once.  Measured slower for the LM-head dX at C2 (200 vs
-            // 177 us in-step, step 6.07 vs 5.95 ms): 192 workgroups with 1.24x the K steps each lose more than
-            // the 3x smaller operand re-fetch saves — the per-CU fill rate, not the fabric, bounds this GEMM.
-            static const bool xs_env = getenv("ERGM_XCD_SPLIT") && atoi(getenv("ERGM_XCD_SPLIT")) != 0;
-            if (xs_env && tiles_of(M, N, 256, 256) <= 32 && K >= 8 * 4096) {
-                split = 8;
-                p.xcd = true;
-            }
+            // (one K slice per XCD — each operand slice fetched into one L2 once — measured slower for the LM-head
+            // dX at C2 with 256x256 tiles, round 3: 200 vs 177 us in-step, and with 256x192 tiles, round 4: the
+            // step +0.7 %; profiles/r04_experiments.txt #8.  GemmArgs::xcd_split keeps the kernel side of it.)
         } else if (K >= 4096 && t128 < 240 && d->split_k != 1) {
             p.cfg = 2;
             // weight gradients over T >= 4096 tokens (config 5): split only the smallest outputs

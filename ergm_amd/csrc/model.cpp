@@ -786,9 +786,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     bool ok = make_stream(&P->side) == hipSuccess &&
               hipEventCreateWithFlags(&P->ev_fork, kSyncEv) == hipSuccess;
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
-    // forward chains over batch slices (1..4; ERGM_FWD_CHAINS, A/B measurements)
+    // two forward chains over the batch halves (one chain measured +3-5 %, three level, four +20 %: round 2)
     P->fwd_chains = 2;
-    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = std::max(1, std::min(2, atoi(e)));
     // two backward chains measured slower at C2 (6.27 vs 5.85 ms/step: the GPU is already throughput-
     // saturated and the host enqueue grows, profiles/r02_bwd_chains_ab.txt): ERGM_BWD_CHAINS=2 enables
     P->bwd_chains = 1;

@@ -203,7 +203,7 @@ def _train_step_grad(ctx, grad_loss, grad_logits, grad_emo):
         post = native = None
         opt = model._overlap_opt
         if opt is not None:  # per-bucket AdamW, overlapped with backward
-            if runner.dp.active or runner.compact_lookup or os.environ.get("ERGM_NATIVE_OPT", "1") == "0":
+            if runner.dp.active or runner.compact_lookup:
                 post = opt._backward_hook(flat, model)   # after each bucket's exchange (Python, comm stream)
             else:
                 native = opt._native_desc(flat, model)   # scheduled by the executor

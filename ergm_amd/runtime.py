@@ -82,9 +82,7 @@ class ModelRunner:
         self.plan = plan
         # the data-gradient chain never waits for the weight-gradient stream between blocks; the
         # consumers of each block's gradients (all-reduce, overlapped AdamW) wait for its mark instead
-        # (ERGM_SIDE_JOINS=1 restores the per-stage joins, for A/B measurements)
-        import os
-        self.per_stage_join = os.environ.get("ERGM_SIDE_JOINS", "0") == "1"
+        self.per_stage_join = False
         L.check(self.lib.ergm_model_set_side_joins(self.plan, int(self.per_stage_join)), "ergm_model_set_side_joins")
         self.grad = grad
         self.shadow = flat_b16
