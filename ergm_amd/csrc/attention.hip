@@ -299,7 +299,7 @@ struct DropBits {
     float scale;
 };
 
-template <bool CAUSAL, bool MASK, bool DROP>
+template <bool CAUSAL, bool MASK, bool DROP, bool PRE = false>
 __device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
                                          int key, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
                                          const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow,
@@ -318,7 +318,7 @@ __device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ql = qb * 16 + 4 * g + r;
-            float pv = exp_sc(s[r], c, sL[ql] * AT_LOG2E);
+            float pv = exp_sc(s[r], c, PRE ? sL[ql] : sL[ql] * AT_LOG2E);  // PRE: sL holds LSE·log2e
             if (MASK) {
                 const int qq = q0 + ql;
                 const bool masked = qq >= Sq || key >= Sk || (CAUSAL && key > qq);
@@ -360,15 +360,15 @@ __device__ __forceinline__ bool dkv_masked(int q0, int Sq, int kw0, int Sk) {
     return q0 + AT_T > Sq || kw0 + 16 > Sk || (CAUSAL && kw0 + 15 > q0);
 }
 
-template <bool CAUSAL, bool DROP>
+template <bool CAUSAL, bool DROP, bool PRE = false>
 __device__ __forceinline__ void dkv_step(const char* sQ, const char* sdO, const float* sL, const float* sD, int q0,
                                          int key, int kw0, int Sq, int Sk, float c, const bf16x8 (&kf)[2],
                                          const bf16x8 (&vf)[2], f32x4 (&dk)[4], f32x4 (&dv)[4], char* tS, int krow,
                                          const DropBits& db) {
     if (dkv_masked<CAUSAL>(q0, Sq, kw0, Sk))
-        dkv_tile<CAUSAL, true, DROP>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
+        dkv_tile<CAUSAL, true, DROP, PRE>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
     else
-        dkv_tile<CAUSAL, false, DROP>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
+        dkv_tile<CAUSAL, false, DROP, PRE>(sQ, sdO, sL, sD, q0, key, Sq, Sk, c, kf, vf, dk, dv, tS, krow, db);
 }
 
 // dQ contribution of one 64-key tile for this lane's query (lq2 = LSE·log2e, dl = δ).  DROP: mword =
@@ -809,7 +809,8 @@ constexpr int AS_OPER = AS_TILES * AT_TILE_BYTES;    // 16 KiB per staged operan
 // fragments — brings it to 83 KiB, room beside one 64-KiB GEMM tile of the concurrent weight-gradient stream; the
 // co-residency measured level at C2 and -1.5 % at C5, profiles/r04_experiments.txt #13.)
 constexpr int AS_DS = AS_TILES * AS_TILES * AT_TILE_BYTES;  // 32 KiB
-constexpr int AS_LDS = 4 * AS_OPER + AS_DS + 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;
+constexpr int AS_SMALL = 2 * AS_MAX * 4 + AS_MAX * AS_TILES * 8;  // LSE, δ, keep bits: 3 KiB
+constexpr int AS_LDS = AS_SMALL + 4 * AS_OPER + AS_DS;
 
 // 128 rows x 64 dims of a token-major operand as two swizzled 64-row tiles (rows >= nrows are zero):
 // the loads are issued first (2 x 16 B per thread), then written to LDS, so several staged operands
@@ -838,25 +839,26 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
 // grid of 32 x 32, v_mfma_f32_16x16x32_bf16, 64-deep K steps through a 2-stage LDS-DMA ring, the same product order as
 // ergm_gemm, so dO is bitwise the c_proj data-gradient GEMM's bf16 output) while Q, K, V and O are loaded, then
 // rounded to bf16 straight into the staged dO tiles — one launch and one HBM round trip fewer on the backward's
-// critical chain, and dO never goes to memory.  The ring occupies K's and V's staging and half of the dS region
-// (48 KiB): K and V are held in registers over the GEMM and staged after it, so the fused form needs no more LDS
-// than the plain one.
+// critical chain, and dO never goes to memory.  The ring occupies the dS region and K's staging (48 KiB): K and V are
+// held in registers over the GEMM and staged after it, so the fused form needs no more LDS than the plain one.
 constexpr int AS_GA = AS_MAX * GEMM_BK * 2;            // 16 KiB: a 128 x 64 gA stage
 constexpr int AS_GW = AT_D * GEMM_BK * 2;              // 8 KiB: a 64 x 64 gW stage
 constexpr int AS_RING = 2 * (AS_GA + AS_GW);           // 48 KiB
-static_assert(AS_RING <= 2 * AS_OPER + AS_DS, "the GEMM ring fits over K's and V's staging and the dS tiles");
+static_assert(AS_RING <= AS_DS + AS_OPER, "the GEMM ring fits over the dS tiles and K's staging");
 
 template <bool CAUSAL, bool DROP, bool GEMM_DO = false>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* sQ = smem;
-    char* sdO = sQ + AS_OPER;
-    char* sK = sdO + AS_OPER;
-    char* sV = sK + AS_OPER;
-    char* sdS = sV + AS_OPER;                          // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
-    float* sL = reinterpret_cast<float*>(sdS + AS_DS);
-    float* sD = sL + AS_MAX;
+    // the per-query arrays first and the most-read tiles next, so their accesses stay within the 64-KiB reach of
+    // the ds_read / ds_write immediate offset (no per-access address arithmetic)
+    float* sL = reinterpret_cast<float*>(smem);        // LSE·log2e per query
+    float* sD = sL + AS_MAX;                           // δ per query
     uint64_t* sM = reinterpret_cast<uint64_t*>(sD + AS_MAX);  // dropout keep bits [query][AS_TILES]
+    char* sQ = smem + AS_SMALL;
+    char* sdO = sQ + AS_OPER;
+    char* sdS = sdO + AS_OPER;                         // tile (kt, qt) at (kt*2 + qt)*8 KiB, [key][query]
+    char* sK = sdS + AS_DS;
+    char* sV = sK + AS_OPER;
     const int b = blockIdx.z, h = blockIdx.y;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i16 = lane & 15, g = lane >> 4;
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         using TA = GldsTile<AS_MAX, false, 8>;
         using TW = GldsTile<AT_D, false, 8>;
         constexpr int LPS = TA::PER_WAVE + TW::PER_WAVE;
-        char* ring = sK;
+        char* ring = sdS;
         const __bf16* gA = a.gA + (size_t)b * a.Sq * a.lda_g;
         const int nk = a.K_g / GEMM_BK;
         auto issue = [&](int kt) {
@@ -953,7 +955,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         dsum += __shfl_xor(dsum, 1, 64);
         dsum += __shfl_xor(dsum, 2, 64);
         if (part == 0) {
-            sL[ql] = lse;
+            sL[ql] = lse * AT_LOG2E;
             sD[ql] = dsum;
         }
     } else {
@@ -994,7 +996,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         dsum += __shfl_xor(dsum, 1, 64);
         dsum += __shfl_xor(dsum, 2, 64);
         if (part == 0) {
-            sL[ql] = lse;
+            sL[ql] = lse * AT_LOG2E;
             sD[ql] = dsum;
         }
     }
@@ -1024,7 +1026,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
             const char* tdO = sdO + qt * AT_TILE_BYTES;
             char* tS = sdS + (kt * AS_TILES + qt) * AT_TILE_BYTES;
             if (DROP) db.mcol = sM + qt * AT_T * AS_TILES + kt;
-            dkv_step<CAUSAL, DROP>(tQ, tdO, sL + qt * AT_T, sD + qt * AT_T, qt * AT_T, key, wave * 16, a.Sq, a.Sk, c, kf,
+            dkv_step<CAUSAL, DROP, true>(tQ, tdO, sL + qt * AT_T, sD + qt * AT_T, qt * AT_T, key, wave * 16, a.Sq, a.Sk, c, kf,
                                    vf, dk, dv, tS, krow, db);
         }
         if (key < a.Sk) {
