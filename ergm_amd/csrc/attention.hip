@@ -318,15 +318,17 @@ __device__ __forceinline__ void dkv_tile(const char* sQ, const char* sdO, const 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ql = qb * 16 + 4 * g + r;
-            float pv = exp_sc(s[r], c, PRE ? sL[ql] : sL[ql] * AT_LOG2E);  // PRE: sL holds LSE·log2e
+            float pv = exp_sc(s[r], c, PRE ? sL[ql] : sL[ql] * AT_LOG2E);  // PRE: sL holds LSE·log2e (short kernel)
             if (MASK) {
                 const int qq = q0 + ql;
                 const bool masked = qq >= Sq || key >= Sk || (CAUSAL && key > qq);
                 pv = masked ? 0.f : pv;
             }
             if constexpr (DROP) {
-                const float z = q0 + ql < Sq ? (((db.mcol[(size_t)ql * db.mstride] >> db.kbit) & 1ull) ? db.scale : 0.f)
-                                             : 0.f;
+                // PRE (the short kernel): its staged keep bits are zero past Sq, so the word is read unguarded
+                const float z = (PRE || q0 + ql < Sq)
+                                    ? (((db.mcol[(size_t)ql * db.mstride] >> db.kbit) & 1ull) ? db.scale : 0.f)
+                                    : 0.f;
                 p[qb][r] = pv * z;
                 ds[qb][r] = pv * (dp[r] * z - sD[ql]);
             } else {
