@@ -841,12 +841,14 @@ __device__ __forceinline__ void put_rows(char* lds, const Rows128& r) {
 // grid of 32 x 32, v_mfma_f32_16x16x32_bf16, 64-deep K steps through a 2-stage LDS-DMA ring, the same product order as
 // ergm_gemm, so dO is bitwise the c_proj data-gradient GEMM's bf16 output) while Q, K, V and O are loaded, then
 // rounded to bf16 straight into the staged dO tiles — one launch and one HBM round trip fewer on the backward's
-// critical chain, and dO never goes to memory.  The ring occupies the dS region and K's staging (48 KiB): K and V are
-// held in registers over the GEMM and staged after it, so the fused form needs no more LDS than the plain one.
+// critical chain, and dO never goes to memory.  The 3-stage ring occupies the dO, dS, K and V staging (72 of 80 KiB):
+// K and V are held in registers over the GEMM and staged after it, and the dO tiles are written once every wave has
+// left the ring, so the fused form needs no more LDS than the plain one.
 constexpr int AS_GA = AS_MAX * GEMM_BK * 2;            // 16 KiB: a 128 x 64 gA stage
 constexpr int AS_GW = AT_D * GEMM_BK * 2;              // 8 KiB: a 64 x 64 gW stage
-constexpr int AS_RING = 2 * (AS_GA + AS_GW);           // 48 KiB
-static_assert(AS_RING <= AS_DS + AS_OPER, "the GEMM ring fits over the dS tiles and K's staging");
+constexpr int AS_GSTAGES = 3;
+constexpr int AS_RING = AS_GSTAGES * (AS_GA + AS_GW);  // 72 KiB
+static_assert(AS_RING <= 3 * AS_OPER + AS_DS, "the GEMM ring fits over the dO, dS, K and V staging");
 
 template <bool CAUSAL, bool DROP, bool GEMM_DO = false>
 __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
@@ -872,15 +874,15 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
         using TA = GldsTile<AS_MAX, false, 8>;
         using TW = GldsTile<AT_D, false, 8>;
         constexpr int LPS = TA::PER_WAVE + TW::PER_WAVE;
-        char* ring = sdS;
+        char* ring = sdO;
         const __bf16* gA = a.gA + (size_t)b * a.Sq * a.lda_g;
         const int nk = a.K_g / GEMM_BK;
         auto issue = [&](int kt) {
-            char* st = ring + (kt & 1) * (AS_GA + AS_GW);
+            char* st = ring + (kt % AS_GSTAGES) * (AS_GA + AS_GW);
             TA::issue(st, gA, a.lda_g, 0, a.Sq, kt * GEMM_BK, wave);
             TW::issue(st + AS_GA, a.gW, a.ldw_g, h * AT_D, a.H * AT_D, kt * GEMM_BK, wave);
         };
-        issue(0);
+        for (int s0 = 0; s0 < AS_GSTAGES - 1 && s0 < nk; ++s0) issue(s0);
         // Q, K, V rows, O for δ and the LSE / keep bits, all in flight beside the GEMM's first stage
         const Rows128 rq = load_rows(Qb, a.ldq, a.Sq);
         const Rows128 rk = load_rows(Kb, a.ldk, a.Sk);
@@ -911,11 +913,11 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int kt = 0; kt < nk; ++kt) {
-            wait_stages<LPS, 0>(0);
+            wait_stages<LPS, AS_GSTAGES - 2>(min(AS_GSTAGES - 2, nk - 1 - kt));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (kt + 1 < nk) issue(kt + 1);
-            const char* st = ring + (kt & 1) * (AS_GA + AS_GW);
+            if (kt + AS_GSTAGES - 1 < nk) issue(kt + AS_GSTAGES - 1);
+            const char* st = ring + (kt % AS_GSTAGES) * (AS_GA + AS_GW);
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 bf16x8 fa[2], fb[2];
@@ -929,6 +931,7 @@ __global__ __launch_bounds__(512) void attn_bwd_short_kernel(AttnArgs a) {
                     for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(fa[i], fb[j], acc[i][j]);
             }
         }
+        __syncthreads();  // every wave is done with the ring, which covers the dO tiles
         // bf16(dO) into the staged tiles: element (row, col) of the C fragment layout (row 4(l>>4) + r, col l & 15)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
