@@ -1155,7 +1155,8 @@ static std::mutex g_over_mu;
 // automatic choice; profiles/r01_step_tune_*.json).  Runtime overrides take precedence.
 static constexpr GemmOverride kStepTuned[] = {
     // config 2 (GPT-2-small, B=16, S=128; forward GEMMs run per batch half, M = 1024)
-    {3073, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // mlp c_proj weight gradient (+ the bias row)
+    {3073, 768, 2048, ERGM_KM, ERGM_KN, 15, 1},  // mlp c_proj weight gradient (+ the bias row); cfg 2 until round 4's
+                                                 // re-tune (profiles/r04_experiments.txt #24)
     {769, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},   // c_attn weight gradient (+ the bias row)
     {3072, 768, 2048, ERGM_KM, ERGM_KN, 2, 1},   // the same with the in-GEMM bias column sums
     {768, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},
