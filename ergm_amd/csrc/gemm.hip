@@ -1162,7 +1162,9 @@ static constexpr GemmOverride kStepTuned[] = {
     {768, 2304, 2048, ERGM_KM, ERGM_KN, 2, 1},
     {1024, 2304, 768, ERGM_MK, ERGM_KN, 3, 1},   // c_attn forward
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
-    {2048, 768, 2304, ERGM_MK, ERGM_NK, 8, 1},   // c_attn data gradient
+    {2048, 768, 2304, ERGM_MK, ERGM_NK, 15, 1},  // c_attn data gradient (cfg 8 until round 4's re-tune)
+    {769, 3072, 2048, ERGM_KM, ERGM_KN, 15, 1},  // c_fc weight gradient (+ the bias row; round 4)
+    {769, 768, 2048, ERGM_KM, ERGM_KN, 11, 1},   // attn c_proj / q / cross c_proj weight gradients (round 4)
     {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
     {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1},
     {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
