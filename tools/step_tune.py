@@ -29,7 +29,10 @@ from ergm_amd import _lib as L  # noqa: E402
 CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13, 22, 23, 24]  # kCfgs indices (gemm.hip)
 TILE = {0: (64, 64), 1: (128, 128), 2: (128, 128), 3: (128, 128), 4: (256, 128), 6: (256, 256), 7: (128, 64),
         8: (64, 128), 9: (256, 128), 10: (128, 128), 11: (64, 64), 12: (128, 64), 13: (64, 128), 14: (128, 128),
-        15: (128, 128), 22: (256, 256), 23: (128, 128), 24: (128, 128)}
+        15: (128, 128), 16: (64, 64), 17: (64, 64), 18: (128, 64), 19: (64, 128), 20: (128, 128), 21: (128, 128),
+        22: (256, 256), 23: (128, 128), 24: (128, 128), 25: (64, 64), 26: (128, 128), 27: (128, 128),
+        28: (256, 256), 29: (64, 128), 30: (128, 128), 31: (128, 128), 32: (128, 128), 33: (64, 64), 34: (64, 64),
+        35: (64, 128), 36: (128, 64), 37: (128, 128)}
 
 
 def main():
@@ -40,6 +43,7 @@ def main():
     ap.add_argument("--max-shapes", type=int, default=24)
     ap.add_argument("--splits", default="1")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
+    ap.add_argument("--candidates", default=None, help="comma-separated kCfgs indices (default: the built-in list)")
     args = ap.parse_args()
     from ergm_amd.config import ERGMConfig
     from ergm_amd.data import synthetic_batch
@@ -108,7 +112,8 @@ def main():
         M, N, K, al, bl = key
         best = None  # None = the automatic choice
         splits = [int(x) for x in args.splits.split(",")]
-        for c, sp in [(c, sp) for sp in splits for c in CANDIDATES]:
+        cands = [int(x) for x in args.candidates.split(",")] if args.candidates else CANDIDATES
+        for c, sp in [(c, sp) for sp in splits for c in cands]:
             bm, bn = TILE[c]
             tiles = -(-M // bm) * -(-N // bn)
             if tiles < 24 or tiles > 20000 or (sp > 1 and (K // sp < 512 or tiles * sp > 2048)):
