@@ -1169,6 +1169,11 @@ static constexpr GemmOverride kStepTuned[] = {
     {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1},
     {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
     {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
+    // config 4 (S = 512, T = 4096), round 4's re-tune (profiles/r04_step_tune_c4.txt, experiments #26)
+    {4096, 3072, 768, ERGM_MK, ERGM_NK, 2, 1},   // mlp c_proj data gradient (GELU' epilogue)
+    {4096, 768, 2304, ERGM_MK, ERGM_NK, 14, 1},  // c_attn data gradient
+    {769, 2304, 4096, ERGM_KM, ERGM_KN, 15, 1},  // c_attn weight gradient (+ the bias row)
+    {769, 768, 4096, ERGM_KM, ERGM_KN, 15, 1},   // E x E weight gradients (+ the bias row)
 };
 
 static bool find_override(const ergm_gemm_desc* d, int& cfg, int& split) {
