@@ -181,12 +181,6 @@ def main():
     ap.add_argument("--torch-metrics", action="store_true",
                     help="per-step metrics with framework ops instead of the executor's loss finalisation")
     ap.add_argument("--backend", default=None, help="torch.distributed backend for N > 1 (default nccl = RCCL)")
-    ap.add_argument("--fuse-optim", action="store_true",
-                    help="single process: AdamW of the block Conv1D weights inside the weight-gradient GEMM epilogues and "
-                         "of the LayerNorm parameters inside their gradient reductions (FusedAdamW(fuse=True)) instead of "
-                         "per-range passes (measured slower at C2, profiles/r04_experiments.txt)")
-    ap.add_argument("--keep-grads", action="store_true",
-                    help="with the fused optimizer, still write the fp32 gradients of the fused ranges")
     ap.add_argument("--defer-update", action="store_true",
                     help="single process: run the block updates after the backward, overlapping the next forward")
     ap.add_argument("--no-gpu-only", dest="gpu_only", action="store_false",
@@ -275,9 +269,7 @@ def main():
     model = GPT2LMHeadModel(cfg, device=dev, process_group=pg)
     model.init_weights(seed=0)
     defer = args.defer_update and world == 1
-    fuse = args.fuse_optim and world == 1 and not args.no_overlap_optim and not defer
-    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim, defer=defer, fuse=fuse,
-                     keep_grads=args.keep_grads or not fuse)
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=not args.no_overlap_optim, defer=defer)
     if args.adamw_blocks is not None:
         opt.overlap_blocks = args.adamw_blocks
     total = args.warmup + args.steps
@@ -511,12 +503,7 @@ def main():
                       "frac": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                       "ceiling_utt_per_s_per_gpu": round(PEAK_BF16_TFLOPS * 1e12 / flops_per_utterance(S, E, Lyr, V),
                                                          0)},
-        "optimizer": "FusedAdamW " + (("fused: every block's Conv1D weights + biases updated in the epilogue of the "
-                                       "weight-gradient GEMM that forms their gradient, LayerNorm parameters in their "
-                                       "gradient reduction, the rest per range overlapped with backward"
-                                       + ("" if opt.keep_grads else " (the fused ranges' fp32 gradients are not "
-                                          "materialised: the update consumes them in registers)")) if fuse else
-                                      (f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks}), "
+        "optimizer": "FusedAdamW " + ((f"per-bucket, overlapped with backward (grid cap {opt.overlap_blocks}), "
                                        + ("scheduled by the native executor" if world == 1 else
                                           "after each bucket's exchange (comm stream)"))
                                       if not args.no_overlap_optim else "after backward"),

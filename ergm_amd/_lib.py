@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 8  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 9  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -32,20 +32,12 @@ class Dropout(C.Structure):
                 ("row0", C.c_int64)]
 
 
-class AdamWEpilogue(C.Structure):
-    """ergm_adamw_epilogue: AdamW in a weight-gradient GEMM's epilogue (ABI 8)."""
-    _fields_ = [("param", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p), ("param_bf16", C.c_void_p),
-                ("write_grad", C.c_int), ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
-                ("weight_decay", C.c_double), ("eps", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float)]
-
-
 class GemmDesc(C.Structure):
     _fields_ = [("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
                 ("ldc", C.c_int), ("a_layout", C.c_int), ("b_layout", C.c_int), ("c_dtype", C.c_int),
                 ("epilogue", C.c_int), ("alpha", C.c_float), ("bias", C.c_void_p), ("aux", C.c_void_p),
                 ("ld_aux", C.c_int), ("aux_out", C.c_void_p), ("ld_aux_out", C.c_int), ("split_k", C.c_int),
-                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p),
-                ("adamw", C.POINTER(AdamWEpilogue))]
+                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p)]
 
 
 class AdamWDesc(C.Structure):
@@ -53,7 +45,7 @@ class AdamWDesc(C.Structure):
                 ("param_bf16", C.c_void_p), ("ranges", C.POINTER(C.c_int64)), ("n_ranges", C.c_int),
                 ("wte_begin", C.c_int64), ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
                 ("weight_decay", C.c_double), ("eps", C.c_float), ("step_size", C.c_float), ("bc2_sqrt", C.c_float),
-                ("max_blocks", C.c_int), ("defer", C.c_int), ("fuse", C.c_int), ("keep_grads", C.c_int)]
+                ("max_blocks", C.c_int), ("defer", C.c_int)]
 
 
 class ModelDims(C.Structure):

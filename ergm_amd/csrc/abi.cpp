@@ -12,8 +12,6 @@ namespace ergm {
 
 static thread_local char g_err[512] = {0};
 thread_local LaunchBind g_bind;  // fork point bound to the next launches (common.h ERGM_LAUNCH)
-thread_local hipStream_t g_watch_s = nullptr;
-thread_local bool g_watch_dirty = true;
 
 void set_error(const char* fmt, ...) {
     va_list ap;

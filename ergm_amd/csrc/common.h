@@ -40,11 +40,6 @@ struct LaunchBind {
     bool bound = false;          // the latest launch on s carries `armed`
 };
 extern thread_local LaunchBind g_bind;
-// a taken fork point stays reusable while nothing is launched on its stream: watch_stream(s) starts watching,
-// ERGM_LAUNCH on the watched stream sets g_watch_dirty
-extern thread_local hipStream_t g_watch_s;
-extern thread_local bool g_watch_dirty;
-inline void watch_stream(hipStream_t s) { g_watch_s = s; g_watch_dirty = false; }
 inline void bind_arm(hipStream_t s, hipEvent_t ev) { g_bind = LaunchBind{s, ev, false}; }
 inline hipEvent_t bind_take(hipStream_t s) {
     hipEvent_t e = (g_bind.armed && g_bind.bound && g_bind.s == s) ? g_bind.armed : nullptr;
@@ -56,7 +51,6 @@ inline void bind_clear() { g_bind = LaunchBind{}; }
 #define ERGM_LAUNCH(K, G, B, SH, S, ...)                                                        \
     do {                                                                                        \
         hipStream_t s_ = (S);                                                                   \
-        if (s_ == ::ergm::g_watch_s) ::ergm::g_watch_dirty = true;                              \
         if (::ergm::g_bind.armed && s_ == ::ergm::g_bind.s) {                                   \
             hipExtLaunchKernelGGL(K, G, B, SH, s_, nullptr, ::ergm::g_bind.armed, 0, __VA_ARGS__); \
             ::ergm::g_bind.bound = true;                                                        \
@@ -167,8 +161,8 @@ __device__ __forceinline__ float gelu_new_grad(float x) {
 // ---- torch.optim.AdamW (src/main.py:68,155), single-tensor algorithm in torch's arithmetic order ----------------
 //   p *= 1 - lr·wd;  m = m + (1-β1)(g - m)  (lerp);  v = β2·v + (1-β2)·g·g  (addcmul)
 //   p += -step_size · m / (sqrt(v)/bc2_sqrt + eps)           (addcdiv)
-// One element.  No FMA contraction: every kernel that applies this update (the optimizer passes of adamw.hip, the
-// weight-gradient GEMM epilogue of gemm.hip, the LayerNorm parameter reduce of norm.hip) must round identically.
+// One element.  No FMA contraction: the optimizer passes of adamw.hip (whole ranges and selected wte rows) must round
+// identically.
 struct AdamScalars {
     float decay, one_m_b1, b2, one_m_b2, eps, step_size, bc2_sqrt;
 };
@@ -186,17 +180,6 @@ __device__ __forceinline__ float adamw_elem(float p, float g, float& m, float& v
 // The scalar products torch forms in double and rounds once when applied to fp32 tensors.
 AdamScalars adam_scalars(double lr, double beta1, double beta2, float eps, double weight_decay, float step_size,
                          float bc2_sqrt);
-
-// AdamW applied where a gradient is formed (GEMM epilogue, LayerNorm reduce): parameter, moments and bf16 shadow
-// at the gradient's own index (`aligned with the gradient`); g_out: also store the gradient (nullptr: don't).
-struct AdamEpi {
-    float* p;       // nullptr: no fused update
-    float* m;
-    float* v;
-    __bf16* sh;     // nullptr: no shadow
-    int write_grad;
-    AdamScalars s;
-};
 
 __device__ __forceinline__ f32x4 ld_nt4(const float* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));

@@ -22,11 +22,6 @@
 
 namespace ergm {
 
-// Internal epilogue code of the AdamW weight-gradient epilogue (ergm_gemm_desc::adamw): its own kernel instantiations,
-// so the parameter / moment registers of the update never weigh on the ordinary epilogues (a runtime branch in every
-// f32 epilogue raised their VGPR counts by up to 2x and cost C5 2-4 %, profiles/r04_experiments.txt #12).
-constexpr int EPI_ADAMW = 64;
-
 
 struct GemmArgs {
     const __bf16* A;
@@ -61,59 +56,7 @@ struct GemmArgs {
     uint8_t* q_out;
     uint8_t* q_sc;
     int ld_q, ld_qs;
-    // weight-gradient GEMMs (KM x KN, EPI_NONE, f32 C): AdamW of the parameters aligned with C in the epilogue
-    // (ergm_adamw_epilogue; opt.p == nullptr: off)
-    AdamEpi opt;
 };
-
-// AdamW epilogue of 8 consecutive gradient values g[0..7] at element idx of C (idx % 8 == 0): parameter, moments
-// and shadow at idx (non-temporal: each is touched once per step), the gradient itself only with write_grad.
-__device__ __forceinline__ void adam_apply8(const AdamEpi& o, float* C, size_t idx, const float* g, const f32x4* pv,
-                                            const f32x4* mv, const f32x4* vv) {
-    f32x4 pn[2], mn[2], vn[2];
-    bf16x8 sb;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float m = mv[h][j], v = vv[h][j];
-            const float x = adamw_elem(pv[h][j], g[4 * h + j], m, v, o.s);
-            pn[h][j] = x;
-            mn[h][j] = m;
-            vn[h][j] = v;
-            sb[4 * h + j] = f2bf(x);
-        }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        st_nt4(o.p + idx + 4 * h, pn[h]);
-        st_nt4(o.m + idx + 4 * h, mn[h]);
-        st_nt4(o.v + idx + 4 * h, vn[h]);
-    }
-    if (o.sh) *reinterpret_cast<bf16x8*>(o.sh + idx) = sb;
-    if (o.write_grad) {
-        st_nt4(C + idx, f32x4{g[0], g[1], g[2], g[3]});
-        st_nt4(C + idx + 4, f32x4{g[4], g[5], g[6], g[7]});
-    }
-}
-__device__ __forceinline__ void adam_store8(const AdamEpi& o, float* C, size_t idx, const float* g) {
-    f32x4 pv[2], mv[2], vv[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        pv[h] = ld_nt4(o.p + idx + 4 * h);
-        mv[h] = ld_nt4(o.m + idx + 4 * h);
-        vv[h] = ld_nt4(o.v + idx + 4 * h);
-    }
-    adam_apply8(o, C, idx, g, pv, mv, vv);
-}
-__device__ __forceinline__ void adam_store1(const AdamEpi& o, float* C, size_t idx, float g) {
-    float m = o.m[idx], v = o.v[idx];
-    const float x = adamw_elem(o.p[idx], g, m, v, o.s);
-    o.p[idx] = x;
-    o.m[idx] = m;
-    o.v[idx] = v;
-    if (o.sh) o.sh[idx] = f2bf(x);
-    if (o.write_grad) C[idx] = g;
-}
 
 template <int EPI, bool OUT_BF16>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, float v) {
@@ -131,10 +74,6 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
         v *= bf2f(reinterpret_cast<const __bf16*>(a.aux)[(size_t)m * a.ld_aux + n]);  // stored gelu'(pre)
     }
     size_t idx = (size_t)m * a.ldc + n;
-    if constexpr (EPI == EPI_ADAMW) {
-        adam_store1(a.opt, reinterpret_cast<float*>(a.C), idx, v);
-        return;
-    }
     if (OUT_BF16) {
         reinterpret_cast<__bf16*>(a.C)[idx] = f2bf(v);
     } else {
@@ -180,10 +119,6 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
         for (int j = 0; j < 8; ++j) v[j] *= bf2f(x[j]);
     }
     const size_t idx = (size_t)m * a.ldc + n;
-    if constexpr (EPI == EPI_ADAMW) {
-        adam_store8(a.opt, reinterpret_cast<float*>(a.C), idx, v);
-        return;
-    }
     if (OUT_BF16) {
         bf16x8 o;
 #pragma unroll
@@ -241,41 +176,6 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
                         t[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
         }
         __syncthreads();
-        if constexpr (EPI == EPI_ADAMW && !OUT_BF16 && !RS && !QMX) {
-            if (!slab) {  // AdamW epilogue: every parameter / moment load of the pass in flight at once
-                constexpr int CPT = (WM * CPR + NT - 1) / NT;
-                f32x4 pv[CPT][2], mv[CPT][2], vv[CPT][2];
-                bool ok[CPT];
-                size_t ix[CPT];
-#pragma unroll
-                for (int i = 0; i < CPT; ++i) {
-                    const int c = threadIdx.x + i * NT;
-                    const int m = m0 + pass * WM + c / CPR, n = n0 + (c % CPR) * 8;
-                    ok[i] = c < WM * CPR && m < a.M && n < a.N;
-                    ix[i] = (size_t)m * a.ldc + n;
-                    if (ok[i]) {
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            pv[i][h] = ld_nt4(a.opt.p + ix[i] + 4 * h);
-                            mv[i][h] = ld_nt4(a.opt.m + ix[i] + 4 * h);
-                            vv[i][h] = ld_nt4(a.opt.v + ix[i] + 4 * h);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < CPT; ++i) {
-                    if (!ok[i]) continue;
-                    const int c = threadIdx.x + i * NT;
-                    const int row = c / CPR, col = (c % CPR) * 8;
-                    const float4 x0 = *reinterpret_cast<const float4*>(t + row * LD + col);
-                    const float4 x1 = *reinterpret_cast<const float4*>(t + row * LD + col + 4);
-                    const float g[8] = {x0.x * alpha, x0.y * alpha, x0.z * alpha, x0.w * alpha,
-                                        x1.x * alpha, x1.y * alpha, x1.z * alpha, x1.w * alpha};
-                    adam_apply8(a.opt, reinterpret_cast<float*>(a.C), ix[i], g, pv[i], mv[i], vv[i]);
-                }
-                continue;
-            }
-        }
         for (int c = threadIdx.x; c < WM * CPR; c += NT) {
             const int row = c / CPR, col = (c % CPR) * 8;
             const int m = m0 + pass * WM + row, n = n0 + col;
@@ -1131,7 +1031,7 @@ static constexpr bool combo_ok(bool akm, bool bkn, int e, bool ob) {
     return (!akm && bkn && (e == ERGM_EPI_BIAS || e == ERGM_EPI_BIAS_GELU) && ob) ||
            (!akm && bkn && e == ERGM_EPI_BIAS_RESID && !ob) || (!akm && bkn && e == ERGM_EPI_NONE && !ob) ||
            (!akm && !bkn && e == ERGM_EPI_NONE) || (!akm && !bkn && e == ERGM_EPI_GELU_BWD && ob) ||
-           (akm && bkn && (e == ERGM_EPI_NONE || e == EPI_ADAMW) && !ob);
+           (akm && bkn && e == ERGM_EPI_NONE && !ob);
 }
 
 static bool pipe_ok(const ergm_gemm_desc* d) {
@@ -1388,10 +1288,6 @@ static void launch_any(const GemmArgs& a, const GemmPlan& p, hipStream_t s) {
 
 template <int EPI, bool OB>
 static void launch_layout(const GemmArgs& a, const GemmPlan& p, int al, int bl, hipStream_t s) {
-    if constexpr (EPI == EPI_ADAMW) {  // validate_desc: weight-gradient layout only
-        launch_any<true, true, EPI, OB>(a, p, s);
-        return;
-    }
     if (al == ERGM_MK && bl == ERGM_NK) launch_any<false, false, EPI, OB>(a, p, s);
     else if (al == ERGM_MK && bl == ERGM_KN) launch_any<false, true, EPI, OB>(a, p, s);
     else if (al == ERGM_KM && bl == ERGM_NK) launch_any<true, false, EPI, OB>(a, p, s);
@@ -1688,11 +1584,6 @@ static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B,
     a.colsum = cs_in ? d->bias_grad : nullptr;
     a.colsum_part = nullptr;
     a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 ? 1 : 0;
-    a.opt = AdamEpi{};
-    if (const ergm_adamw_epilogue* o = d->adamw) {
-        a.opt = AdamEpi{o->param, o->exp_avg, o->exp_avg_sq, reinterpret_cast<__bf16*>(o->param_bf16), o->write_grad,
-                        adam_scalars(o->lr, o->beta1, o->beta2, o->eps, o->weight_decay, o->step_size, o->bc2_sqrt)};
-    }
     return a;
 }
 }  // namespace ergm
@@ -1729,15 +1620,6 @@ static int validate_desc(const ergm_gemm_desc* d, const void* A, const void* B, 
     ERGM_CHECK_ARG(!d->bias_grad || (d->a_layout == ERGM_KM && d->b_layout == ERGM_KN && e == ERGM_EPI_NONE &&
                                      d->c_dtype == ERGM_F32),
                    "ergm_gemm: bias_grad needs a_layout KM, b_layout KN, epilogue NONE and f32 C");
-    if (const ergm_adamw_epilogue* o = d->adamw) {
-        ERGM_CHECK_ARG(d->a_layout == ERGM_KM && d->b_layout == ERGM_KN && e == ERGM_EPI_NONE &&
-                           d->c_dtype == ERGM_F32 && !d->bias_grad,
-                       "ergm_gemm: the AdamW epilogue needs a_layout KM, b_layout KN, epilogue NONE, f32 C, no bias_grad");
-        ERGM_CHECK_ARG(o->param && o->exp_avg && o->exp_avg_sq, "ergm_gemm: AdamW epilogue: null parameter / moments");
-        ERGM_CHECK_ARG(aligned16(o->param) && aligned16(o->exp_avg) && aligned16(o->exp_avg_sq) &&
-                           (!o->param_bf16 || aligned16(o->param_bf16)) && aligned16(C),
-                       "ergm_gemm: AdamW epilogue: 16-byte alignment of C, parameters, moments and shadow");
-    }
 
     return ERGM_OK;
 }
@@ -1769,11 +1651,6 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
             else launch_reduce<E, false>(a, p.split, s);                   \
         }                                                                 \
         break;
-    if (d->adamw) {  // the AdamW epilogue: its own instantiations (validate_desc: KM x KN, f32 C)
-        launch_layout<EPI_ADAMW, false>(a, p, d->a_layout, d->b_layout, s);
-        if (p.split > 1) launch_reduce<EPI_ADAMW, false>(a, p.split, s);
-        return check_launch("ergm_gemm");
-    }
     switch (e) {
         ERGM_EPI_CASE(ERGM_EPI_NONE)
         ERGM_EPI_CASE(ERGM_EPI_BIAS)
@@ -1812,7 +1689,6 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
             d[i]->c_dtype != ERGM_F32 || d[i]->split_k > 1 || !pipe_ok(d[i]))
             return ERGM_EUNSUPPORTED;
     }
-    if ((d[0]->adamw == nullptr) != (d[1]->adamw == nullptr)) return ERGM_EUNSUPPORTED;  // one epilogue per launch
     GemmPlan p[2] = {plan_gemm(d[0]), plan_gemm(d[1])};
     const int cfg = p[0].cfg;
     if (cfg < 0 || (cfg >= 16 && kCfgs[cfg].il == 0) || kCfgs[cfg].ks != 1 || p[1].cfg != cfg || p[0].split != 1 ||
@@ -1832,13 +1708,6 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
     g.b1 = (n0 + 7) & ~7;
     const int nb = g.b1 + n1;
     hipStream_t s = as_stream(stream);
-    if (d[0]->adamw) {  // AdamW epilogue pairs: the configurations the executor's block pairs plan to
-        if (cfg == 0) launch_dw2_cfg<0, EPI_ADAMW>(g, nb, s);
-        else if (cfg == 2) launch_dw2_cfg<2, EPI_ADAMW>(g, nb, s);
-        else if (cfg == 10) launch_dw2_cfg<10, EPI_ADAMW>(g, nb, s);
-        else return ERGM_EUNSUPPORTED;
-        return check_launch("gemm_dw_pair");
-    }
     switch (cfg) {
         case 0: launch_dw2_cfg<0>(g, nb, s); break;
         case 1: launch_dw2_cfg<1>(g, nb, s); break;

@@ -53,8 +53,7 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
-                             float* const* dgamma, float* const* dbeta, hipStream_t s, const float* gbase,
-                             const AdamEpi* opt);
+                             float* const* dgamma, float* const* dbeta, hipStream_t s);
 int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
                           const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
                           const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s);
@@ -100,7 +99,6 @@ struct DwJob {
     float* gW;
     float* gB;
     int ldc;  // row stride of gW (N, or the stacked matrix's width for a column slice)
-    bool fuse;  // a block Conv1D: the fused optimizer updates [W; b] in the GEMM's epilogue
 };
 
 struct ergm_model_plan {
@@ -189,10 +187,7 @@ struct ergm_model_plan {
     // Two HIP streams: the caller's stream runs the critical chain; `side` runs weight-gradient GEMMs
     // (and the stacked caption K/V GEMM in forward), forked/joined with events.
     hipStream_t side;
-    hipEvent_t ev_fork;
-    // fork points are bound to the producing launch (common.h ERGM_LAUNCH)
-    hipEvent_t pt_ev = nullptr;  // the last fork point taken on pt_s, reusable while nothing is launched there
-    hipStream_t pt_s = nullptr;
+    hipEvent_t ev_fork;  // fork points are bound to the producing launch (common.h ERGM_LAUNCH) or recorded
     std::vector<hipEvent_t> ev_join;  // one per backward stage (L layers + head + embed)
     // inputs
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
@@ -225,8 +220,6 @@ struct ergm_model_plan {
     // executor-scheduled AdamW (ergm_model_set_optimizer): descriptor copy, its ranges, the optimizer stream
     // and the main-stream marks it waits for (one per update of a step)
     bool opt_on;
-    bool opt_fuse;  // opt.fuse in effect: block Conv1D weights and LayerNorm parameters updated where their
-                    // gradients are formed (dW epilogue, LayerNorm reduce)
     ergm_adamw_desc opt;
     std::vector<int64_t> opt_ranges;
     hipStream_t opt_s;
@@ -463,15 +456,12 @@ hipError_t make_stream(hipStream_t* s) { return hipStreamCreateWithFlags(s, hipS
 constexpr unsigned kSyncEv = hipEventDisableTiming | hipEventDisableSystemFence;
 
 // An event that completes with everything enqueued so far on `s`: the fork point armed before the stage's last
-// launch on s when that launch carried it (arm_fork: no marker packet on s), else `ev` recorded on s.
+// launch on s when that launch carried it and nothing else was enqueued on s since (arm_fork: no marker packet on
+// s), else `ev` recorded on s.  The caller waits on it at once: ev_fork is re-bound by the next arm.
 hipEvent_t stream_point(ergm_model_plan* P, hipStream_t s, hipEvent_t ev) {
+    (void)P;
     hipEvent_t e = bind_take(s);
-    // the previous point of s, when nothing was launched (or joined) on s since it was taken
-    if (!e && P->pt_ev && P->pt_s == s && g_watch_s == s && !g_watch_dirty && !P->per_stage_join) e = P->pt_ev;
     if (!e && hipEventRecord(ev, s) == hipSuccess) e = ev;
-    P->pt_ev = e;
-    P->pt_s = s;
-    watch_stream(s);
     return e;
 }
 // Bind the next fork point of `s` to the launches that follow on s (the stage's producer of the fork).
@@ -533,47 +523,24 @@ struct LaunchClass {
     ~LaunchClass() { P->launch_cls = prev; }
 };
 
-// The fused optimizer's update of the parameters whose gradient lives at `g` (ergm_adamw_epilogue: parameter,
-// moments and shadow aligned with the gradient; ergm_model_set_optimizer's descriptor).
-ergm_adamw_epilogue adamw_at(const ergm_model_plan* P, const float* g) {
-    const ergm_adamw_desc& o = P->opt;
-    const ptrdiff_t off = g - o.grad;
-    ergm_adamw_epilogue e{};
-    e.param = o.param + off;
-    e.exp_avg = o.exp_avg + off;
-    e.exp_avg_sq = o.exp_avg_sq + off;
-    e.param_bf16 = o.param_bf16 ? reinterpret_cast<__bf16*>(o.param_bf16) + off : nullptr;
-    e.write_grad = o.keep_grads;
-    e.lr = o.lr; e.beta1 = o.beta1; e.beta2 = o.beta2; e.weight_decay = o.weight_decay;
-    e.eps = o.eps; e.step_size = o.step_size; e.bc2_sqrt = o.bc2_sqrt;
-    return e;
-}
-
 // Weight gradient of a Conv1D: gW[M][N] = Aᵀ·dY over the T tokens (A = the layer input, [T][lda]) and its
 // bias gradient gB[N] = Σ_t dY[t][n].  With fused_bias the A operand's column M is all ones and gB == gW + M·N,
 // so one GEMM over M+1 rows writes [gW; gB] (the extra tile row runs beside the others); otherwise the GEMM
 // sums gB from the dY fragments it stages (ergm_gemm_desc.bias_grad: measured equal at C2 but +4 % step time
 // at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
-// With the fused optimizer (P->opt_fuse, job.fuse: a block's Conv1D) the GEMM's epilogue also applies AdamW to
-// [W; b] (ergm_adamw_epilogue) instead of leaving it to a pass over the range.
 double dw_flops(const ergm_model_plan* P, const DwJob& j) { return 2.0 * j.M * j.N * P->T + (double)j.N * P->T; }
-void dw_desc(const ergm_model_plan* P, const DwJob& j, ergm_gemm_desc& g, ergm_adamw_epilogue& ae) {
+void dw_desc(const ergm_model_plan* P, const DwJob& j, ergm_gemm_desc& g) {
     memset(&g, 0, sizeof(g));
     g.M = P->fused_bias ? j.M + 1 : j.M;
     g.N = j.N; g.K = P->T; g.lda = j.lda; g.ldb = j.ldy; g.ldc = j.ldc;
     g.a_layout = ERGM_KM; g.b_layout = ERGM_KN; g.c_dtype = ERGM_F32; g.epilogue = ERGM_EPI_NONE;
     g.alpha = 1.0f;
     g.bias_grad = P->fused_bias ? nullptr : j.gB;
-    if (j.fuse && P->opt_fuse && !P->dry) {
-        ae = adamw_at(P, j.gW);
-        g.adamw = &ae;
-    }
 }
 int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
     Probe pr(P, 5, s, dw_flops(P, j));
     ergm_gemm_desc g;
-    ergm_adamw_epilogue ae;
-    dw_desc(P, j, g, ae);
+    dw_desc(P, j, g);
     const size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
     if (P->dry) return ERGM_OK;
@@ -585,9 +552,8 @@ int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
 int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJob& j1) {
     if (!P->dw_group) return ERGM_EUNSUPPORTED;
     ergm_gemm_desc g[2];
-    ergm_adamw_epilogue ae[2];
-    dw_desc(P, j0, g[0], ae[0]);
-    dw_desc(P, j1, g[1], ae[1]);
+    dw_desc(P, j0, g[0]);
+    dw_desc(P, j1, g[1]);
     const ergm_gemm_desc* d[2] = {&g[0], &g[1]};
     const void* A[2] = {j0.A, j1.A};
     const void* B[2] = {j0.dY, j1.dY};
@@ -597,10 +563,10 @@ int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJ
     return gemm_dw_pair(d, A, B, C, s, true);
 }
 // Queue a weight-gradient GEMM; dw_flush launches the queue on the side stream behind ONE fork from the data-
-// gradient chain(s).  fuse: a block Conv1D whose update the fused optimizer applies in the epilogue.
+// gradient chain(s).
 int dw_gemm(ergm_model_plan* P, const Chains& ch, int M, int N, const __bf16* A, int lda, const __bf16* dY, int ldy,
-            float* gW, float* gB, bool fuse, int ldc = 0) {
-    const DwJob j{M, N, A, lda, dY, ldy, gW, gB, ldc ? ldc : N, fuse};
+            float* gW, float* gB, int ldc = 0) {
+    const DwJob j{M, N, A, lda, dY, ldy, gW, gB, ldc ? ldc : N};
     if (P->dry) return dw_launch(P, ch.s[0], j);
     P->dw_pend.push_back(j);
     return ERGM_OK;
@@ -655,21 +621,12 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
     return ln_reduce_add(P, slot, dgamma, dbeta);
 }
 
-// With the fused optimizer the reduce also applies AdamW to γ / β from their final gradients (the LayerNorm's own
-// backward, the only reader of γ in the backward, has run: the reduce is forked behind it).
 int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
     if (P->dry || P->ln_pending == 0) return ERGM_OK;
     ERGM_TRY(fork_side(P, ch));
     const int n = P->ln_pending;
     P->ln_pending = 0;
-    AdamEpi ae{};
-    if (P->opt_fuse) {
-        const ergm_adamw_desc& o = P->opt;
-        ae = AdamEpi{o.param, o.exp_avg, o.exp_avg_sq, reinterpret_cast<__bf16*>(o.param_bf16), o.keep_grads,
-                     adam_scalars(o.lr, o.beta1, o.beta2, o.eps, o.weight_decay, o.step_size, o.bc2_sqrt)};
-    }
-    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side,
-                                    P->opt.grad, P->opt_fuse ? &ae : nullptr);
+    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
 }
 
 
@@ -854,7 +811,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->probe = 0;
     P->launch_cls = 0;
     P->opt_on = false;
-    P->opt_fuse = false;
     P->opt_s = nullptr;
     P->opt_k = 0;
     P->ev_begin = P->ev_end = nullptr;
@@ -1297,6 +1253,7 @@ extern "C" int ergm_model_forward(ergm_model_plan* P, void* logits, float* emo_l
     ERGM_CHECK_ARG(P && logits && emo_logits, "model_forward: null argument");
     ERGM_CHECK_ARG(P->ids, "model_forward: call ergm_model_set_inputs first");
     ERGM_CHECK_ARG(!(P->labels || P->emo_labels) || out_loss, "model_forward: labels need out_loss");
+    bind_clear();  // a fork point is armed and taken inside one native call
     return do_forward(P, logits, emo_logits, out_loss, train, as_stream(stream));
 }
 
@@ -1374,35 +1331,29 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
     auto Tc = [&](int c) { return ch.nb[c] * S; };
     // Weight-gradient pairs (mlp c_proj + c_fc, cross c_proj + q, attn c_proj + c_attn) are forked to the side
-    // stream once the dY of the second member is formed.  With the fused optimizer their epilogues rewrite the
-    // weights' bf16 shadow, so the fork comes after the second member's data-gradient GEMM instead — the last
-    // reader of that shadow in this backward (the first member's is already behind the fork point).
-    const bool late = P->opt_fuse;
+    // stream once the dY of the second member is formed.
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
     // fork's event itself (arm_fork before it) instead of a marker packet recorded behind it
     const bool arm = ch.n == 1 && !P->dry;
     // ---- MLP: x3 = x2 + drop(gelu(ln2(x2)·Wfc + bfc)·Wm + bm)
-    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B), true));
-    if (arm && !late) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
+    ERGM_TRY(dw_gemm(P, ch, F, E, a.act, P->XF, dh3, E, LG(P, l, ERGM_T_MPROJ_W), LG(P, l, ERGM_T_MPROJ_B)));
+    if (arm) arm_fork(P, s);  // dpre (mlp c_proj dX with GELU'): the c_fc dW's dY
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), F, E, R(dh3, c, E), E, ERGM_MK, LB(P, l, ERGM_T_MPROJ_W), E, ERGM_NK,
                       R(dpre, c, F), F, ERGM_BF16, ERGM_EPI_GELU_BWD, nullptr, R(a.pre, c, F), F));
-    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B), true));
-    if (!late) ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
-    for (int c = 0; c < ch.n; ++c) {
-        if (arm && late) arm_fork(P, s);  // the c_fc dX: the last reader of W_fc
+    ERGM_TRY(dw_gemm(P, ch, E, F, a.ln2, P->XE, dpre, F, LG(P, l, ERGM_T_FC_W), LG(P, l, ERGM_T_FC_B)));
+    ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
+    for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-    }
-    if (late) ERGM_TRY(dw_flush(P, ch));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
     // ---- cross-attention: x2 = x1 + drop(Attn(ln_x(x1)·Wq + bq, KV_l(cap))·Wxp + bxp)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B), true));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.xo, P->XE, dh2, E, LG(P, l, ERGM_T_XPROJ_W), LG(P, l, ERGM_T_XPROJ_B)));
     for (int c = 0; c < ch.n; ++c) {
         if (P->attn_fuse && ch.nb[c] * H <= kAttnFuseMaxWg) {  // dO = dh2·Wxpᵀ formed inside the attention backward
-            if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
+            if (arm) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
             if (!P->dry) {
                 const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
                 __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1417,7 +1368,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh2, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XPROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm && !late) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
+        if (arm) arm_fork(P, s);  // the cross-attention backward: dxq, the q dW's dY
         if (!P->dry) {
             const __bf16* kl = R(P->kv_all, c, L2E) + (size_t)l * 2 * E;
             __bf16* dkl = R(P->dkv_all, c, L2E) + (size_t)l * 2 * E;
@@ -1428,22 +1379,19 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    E, E, L2E, L2E, 0, &dp, attn_bits(P, l, 1, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B), true));
-    if (!late) ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
-    for (int c = 0; c < ch.n; ++c) {
-        if (arm && late) arm_fork(P, s);  // the q dX: the last reader of W_q
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.lnx, P->XE, dxq, E, LG(P, l, ERGM_T_XQ_W), LG(P, l, ERGM_T_XQ_B)));
+    ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
+    for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
                       R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-    }
-    if (late) ERGM_TRY(dw_flush(P, ch));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
     // ---- self-attention: x1 = x0 + drop(Attn(ln_1(x0)·Wqkv + b)·Wap + bap)
-    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B), true));
+    ERGM_TRY(dw_gemm(P, ch, E, E, a.ao, P->XE, dh1, E, LG(P, l, ERGM_T_APROJ_W), LG(P, l, ERGM_T_APROJ_B)));
     for (int c = 0; c < ch.n; ++c) {
         if (P->attn_fuse && ch.nb[c] * H <= kAttnFuseMaxWg) {  // dO = dh1·Wapᵀ formed inside the attention backward
-            if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
+            if (arm) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
             if (!P->dry) {
                 const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
                 const size_t bhs = (size_t)ch.b0[c] * H * S;
@@ -1458,7 +1406,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
         }
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dh1, c, E), E, ERGM_MK, LB(P, l, ERGM_T_APROJ_W), E, ERGM_NK,
                       R(P->d_o, c, E), E, ERGM_BF16, ERGM_EPI_NONE));
-        if (arm && !late) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
+        if (arm) arm_fork(P, s);  // the self-attention backward: dqkv, the c_attn dW's dY
         if (!P->dry) {
             const ergm_dropout dp = attn_drop(P, l, 0, ch.b0[c]);
             const size_t bhs = (size_t)ch.b0[c] * H * S;
@@ -1469,15 +1417,11 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
                                    3 * E, 3 * E, 1, &dp, attn_bits(P, l, 0, ch.b0[c]), ch.s[c]));
         }
     }
-    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B),
-                     true));
-    if (!late) ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
-    for (int c = 0; c < ch.n; ++c) {
-        if (arm && late) arm_fork(P, s);  // the c_attn dX: the last reader of W_qkv
+    ERGM_TRY(dw_gemm(P, ch, E, 3 * E, a.ln1, P->XE, dqkv, 3 * E, LG(P, l, ERGM_T_ATTN_W), LG(P, l, ERGM_T_ATTN_B)));
+    ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
+    for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
                       ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
-    }
-    if (late) ERGM_TRY(dw_flush(P, ch));
     for (int c = 0; c < ch.n; ++c) {
         if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));
@@ -1525,7 +1469,7 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
     {  // the stacked caption K/V projection: dW = capᵀ·dKV_all (side), dcap = dKV_all·Wᵀ (main), one GEMM each
         // (per block instead, in the block stages: 0.25 ms/step slower at C2, profiles/r03_experiments.txt #6)
         const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
-        ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b, false));
+        ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
         ERGM_TRY(dw_flush(P, one));
         ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                       ERGM_EPI_NONE));
@@ -1549,7 +1493,6 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
     ERGM_CHECK_ARG(P, "model_set_optimizer: null plan");
     if (!o) {
         P->opt_on = false;
-        P->opt_fuse = false;
         return ERGM_OK;
     }
     const int L = P->d.n_layer;
@@ -1560,11 +1503,6 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
                            o->ranges[2 * k] % 4 == 0 && o->ranges[2 * k + 1] % 4 == 0,
                        "model_set_optimizer: range %d must be non-empty, 4-element aligned", k);
     ERGM_CHECK_ARG(o->wte_begin >= 0 && o->wte_begin % 4 == 0, "model_set_optimizer: bad wte_begin");
-    ERGM_CHECK_ARG(!o->fuse || (!o->defer && P->fused_bias && aligned16(o->param) && aligned16(o->exp_avg) &&
-                                aligned16(o->exp_avg_sq) && aligned16(o->grad) &&
-                                (!o->param_bf16 || aligned16(o->param_bf16))),
-                   "model_set_optimizer: fuse needs defer = 0, every Conv1D bias right after its weight and 16-byte "
-                   "aligned buffers");
     if (!P->opt_s) {
         if (make_stream(&P->opt_s) != hipSuccess)
             return fail(ERGM_EHIP, "model_set_optimizer: stream creation");
@@ -1580,21 +1518,22 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
     P->opt_ranges.assign(o->ranges, o->ranges + 2 * (L + 1));
     P->opt.ranges = P->opt_ranges.data();
     P->opt_on = true;
-    P->opt_fuse = o->fuse != 0;
     return ERGM_OK;
 }
 
 namespace {
-// The optimizer stream waits for the work issued so far on `s` and, unless the stages already join the
-// side stream, for the side stream's weight-gradient mark `mark` (< 0: none).
+// The optimizer stream waits for a bucket's gradients and for the last reader of its parameters.  mark >= 0: the
+// side stream's mark of that stage (a block l, L+1 = the LM-head dW) — recorded behind the stage's final fork from
+// the data-gradient chain(s) (the LayerNorm reduce after ln_1's backward; the LM-head dW after the LM-head dX),
+// so it also covers every data-gradient launch of the stage, on every chain.  mark < 0: everything issued so far
+// on `s` (a fresh event).
 int opt_wait(ergm_model_plan* P, hipStream_t s, int mark) {
+    if (mark >= 0)
+        return hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) == hipSuccess
+                   ? ERGM_OK
+                   : fail(ERGM_EHIP, "model: optimizer stream wait");
     hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
-    // the stage's last fork point, when nothing was launched (or joined) on s since it was taken
-    const bool reuse = P->pt_ev && P->pt_s == s && g_watch_s == s && !g_watch_dirty && !P->per_stage_join;
-    if (reuse) e = P->pt_ev;
-    if ((!reuse && hipEventRecord(e, s) != hipSuccess) || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
-        return fail(ERGM_EHIP, "model: optimizer stream wait");
-    if (mark >= 0 && hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) != hipSuccess)
+    if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
         return fail(ERGM_EHIP, "model: optimizer stream wait");
     return ERGM_OK;
 }
@@ -1623,14 +1562,6 @@ int opt_after_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // -0.6 %, C4 equal; lag 0 slower).
     const int lag = P->opt_lag;
     auto upd = [&](int m) -> int {
-        if (P->opt_fuse) {
-            // fused: a block's Conv1D weights and LayerNorm parameters (ln_f's too) were updated where their gradients
-            // were formed; of bucket 0 (head + block L-1) the emotion head is left
-            if (m != L - 1) return ERGM_OK;
-            ERGM_TRY(opt_wait(P, s, m));
-            const int64_t a = P->p.g_emo_w - P->opt.grad;
-            return opt_range(P, a, a + (int64_t)7 * P->d.n_embd);
-        }
         ERGM_TRY(opt_wait(P, s, m));
         return opt_range(P, P->opt.ranges[2 * (L - 1 - m)], P->opt.ranges[2 * (L - 1 - m) + 1]);
     };
@@ -1687,12 +1618,14 @@ extern "C" int ergm_model_optimizer_join(ergm_model_plan* P, void* stream) {
 extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_head: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_head: no training forward to differentiate");
+    bind_clear();
     return do_backward_head(P, gscale, as_stream(stream));
 }
 
 extern "C" int ergm_model_backward_layer(ergm_model_plan* P, int layer, void* stream) {
     ERGM_CHECK_ARG(P && layer >= 0 && layer < P->d.n_layer, "model_backward_layer: bad layer");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_layer: no training forward to differentiate");
+    bind_clear();
     ERGM_TRY(do_backward_layer(P, layer, as_stream(stream)));
     return opt_after_layer(P, layer, as_stream(stream));
 }
@@ -1700,6 +1633,7 @@ extern "C" int ergm_model_backward_layer(ergm_model_plan* P, int layer, void* st
 extern "C" int ergm_model_backward_embed(ergm_model_plan* P, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_embed: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_embed: no training forward to differentiate");
+    bind_clear();
     ERGM_TRY(do_backward_embed(P, as_stream(stream)));
     return opt_after_embed(P, as_stream(stream));
 }

@@ -248,10 +248,6 @@ struct LnReduceJobs {  // up to 4 LayerNorms' (partials, dγ, dβ) reduced by on
     const float* part_b[4];
     float* dgamma[4];
     float* dbeta[4];
-    // optional AdamW of γ / β (the executor's fused optimizer): opt's parameter / moment / shadow bases are aligned
-    // with gbase, the flat gradient buffer dγ and dβ live in (opt.p == nullptr: off)
-    const float* gbase;
-    AdamEpi opt;
 };
 
 // 256-thread blocks (32 columns x 8 row lanes, 16 partial rows in flight per lane): small enough to
@@ -288,19 +284,7 @@ __global__ __launch_bounds__(256) void ln_param_reduce_kernel(LnReduceJobs jobs,
         for (int w = 1; w < 8; w <<= 1)
 #pragma unroll
             for (int j = 0; j < 8; j += 2 * w) t[j] += t[j + w];
-        const AdamEpi& o = jobs.opt;
-        if (o.p) {  // the update of this γ / β element from its final gradient (adamw_elem: ergm_adamw_step's rounding)
-            const size_t i = (size_t)(out + c - jobs.gbase);
-            float m = o.m[i], v = o.v[i];
-            const float x = adamw_elem(o.p[i], t[0], m, v, o.s);
-            o.p[i] = x;
-            o.m[i] = m;
-            o.v[i] = v;
-            if (o.sh) o.sh[i] = f2bf(x);
-            if (o.write_grad) out[c] = t[0];
-        } else {
-            out[c] = t[0];
-        }
+        out[c] = t[0];
     }
 }
 
@@ -468,14 +452,9 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
 }
 
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
-                             float* const* dgamma, float* const* dbeta, hipStream_t s, const float* gbase,
-                             const AdamEpi* opt) {
+                             float* const* dgamma, float* const* dbeta, hipStream_t s) {
     ERGM_CHECK_ARG(n >= 1 && n <= 4, "layernorm_param_reduce: 1..4 jobs per launch");
     LnReduceJobs j{};
-    if (opt && opt->p) {
-        j.gbase = gbase;
-        j.opt = *opt;
-    }
     for (int i = 0; i < n; ++i) {
         ERGM_CHECK_ARG(part_g[i] && part_b[i] && dgamma[i] && dbeta[i], "layernorm_param_reduce: null argument");
         j.part_g[i] = part_g[i]; j.part_b[i] = part_b[i]; j.dgamma[i] = dgamma[i]; j.dbeta[i] = dbeta[i];
@@ -486,7 +465,7 @@ int layernorm_param_reduce_n(int n, const float* const* part_g, const float* con
 
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s) {
-    return layernorm_param_reduce_n(1, &part_g, &part_b, rows, E, &dgamma, &dbeta, s, nullptr, nullptr);
+    return layernorm_param_reduce_n(1, &part_g, &part_b, rows, E, &dgamma, &dbeta, s);
 }
 }  // namespace ergm
 

@@ -34,7 +34,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-
+import warnings
 import weakref
 from collections import OrderedDict
 from dataclasses import dataclass
@@ -153,6 +153,9 @@ def _(flat, grad_loss, grad_logits, handle, key):
     return torch.empty_like(flat)
 
 
+_warned_compiled_logits = [False]
+
+
 def _train_step_setup(ctx, inputs, output):
     handle, key = inputs[8], inputs[9]
     ctx.handle, ctx.key = handle, key
@@ -161,6 +164,11 @@ def _train_step_setup(ctx, inputs, output):
     ctx.mark_non_differentiable(output[2])
     if model is not None and _compiling(output[0]) and not model.compiled_logits_grad:
         ctx.mark_non_differentiable(output[1])
+        if not _warned_compiled_logits[0]:  # a loss on the compiled logits would silently lose its term
+            _warned_compiled_logits[0] = True
+            warnings.warn("ergm: under torch.compile the returned logits are non-differentiable (a loss term built on "
+                          "them contributes no gradient); set GPT2LMHeadModel.compiled_logits_grad = True BEFORE "
+                          "compiling to differentiate through them (the flag is read at trace time)", stacklevel=2)
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(inputs[0])
 

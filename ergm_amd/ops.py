@@ -33,12 +33,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int
          out: Optional[torch.Tensor] = None, out_dtype=torch.float32, epilogue: int = L.EPI_NONE,
          bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
          aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0, split_k: int = 0,
-         alpha_dev: Optional[torch.Tensor] = None, bias_grad: Optional[torch.Tensor] = None,
-         adamw: Optional[dict] = None) -> torch.Tensor:
+         alpha_dev: Optional[torch.Tensor] = None, bias_grad: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C[M,N] = epilogue(alpha · A·B); A/B bf16 row-major with layouts as in ergm_hip.h.  ``bias_grad`` (f32 [N],
-    KM x KN weight gradients only) also receives alpha·Σ_k B[k][n].  ``adamw`` (KM x KN weight gradients only):
-    dict(param, exp_avg, exp_avg_sq, shadow=None, write_grad=True, lr, betas, eps, weight_decay, step) — the AdamW
-    update of the parameters (laid out like C) in the GEMM's epilogue (ergm_adamw_epilogue)."""
+    KM x KN weight gradients only) also receives alpha·Σ_k B[k][n]."""
     _need_gpu(A, B)
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
     lda = A.stride(0) if A.dim() == 2 else (K if a_layout == L.MK else M)
@@ -50,16 +47,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int
                    bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
                    aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0,
                    split_k=split_k, alpha_dev=_ptr(alpha_dev), bias_grad=_ptr(bias_grad))
-    if adamw is not None:
-        b1, b2 = adamw.get("betas", (0.9, 0.999))
-        t, lr = adamw["step"], adamw["lr"]
-        sh = adamw.get("shadow")
-        ae = L.AdamWEpilogue(param=_ptr(adamw["param"]), exp_avg=_ptr(adamw["exp_avg"]),
-                             exp_avg_sq=_ptr(adamw["exp_avg_sq"]), param_bf16=_ptr(sh),
-                             write_grad=int(adamw.get("write_grad", True)), lr=lr, beta1=b1, beta2=b2,
-                             weight_decay=adamw.get("weight_decay", 1e-2), eps=adamw.get("eps", 1e-8),
-                             step_size=lr / (1 - b1 ** t), bc2_sqrt=math.sqrt(1 - b2 ** t))
-        d.adamw = C.pointer(ae)
     lib = L.load()
     wsb = lib.ergm_gemm_workspace_size(C.byref(d))
     ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=A.device)

@@ -98,17 +98,10 @@ class FusedAdamW(torch.optim.Optimizer):
     src/main.py:152-156, no gradient clipping in between), and ``step()`` only advances the step count.  Each backward applies one update, so this mode is for loops that
     call ``backward()`` once per ``step()`` (the reference's); gradient accumulation (a backward onto
     an existing ``.grad``) falls back to updating in ``step()``.
-
-    ``fuse=True`` (single process, with ``overlap``): every block's Conv1D weights and biases are updated inside
-    the epilogue of the weight-gradient GEMM that forms their gradient, and every LayerNorm's γ / β inside the
-    reduction that forms theirs (``ergm_adamw_desc.fuse``) — the same arithmetic, bit for bit, without a
-    separate pass over those 56 % of the parameters.  ``keep_grads=False`` additionally skips writing their
-    fp32 gradients (``flat.grad`` then holds stale values for those ranges after the backward; the
-    reference loop never reads them, src/main.py:152-156).
     """
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 model=None, overlap: bool = False, defer: bool = False, fuse: bool = False, keep_grads: bool = True):
+                 model=None, overlap: bool = False, defer: bool = False):
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         if not 0.0 <= eps:
@@ -122,10 +115,6 @@ class FusedAdamW(torch.optim.Optimizer):
         # single process, overlap=True: the block updates run after the backward, overlapping the next
         # forward (which waits for each block's update before that block; ergm_model_optimizer_join)
         self.defer = bool(defer)
-        if fuse and (not overlap or defer):
-            raise ValueError("fuse=True needs overlap=True and defer=False")
-        self.fuse = bool(fuse)
-        self.keep_grads = bool(keep_grads)
         if overlap:
             if model is None:
                 raise ValueError("overlap=True needs model=")
@@ -202,8 +191,6 @@ class FusedAdamW(torch.optim.Optimizer):
         d.bc2_sqrt = math.sqrt(1 - b2 ** t)
         d.max_blocks = int(self.overlap_blocks)
         d.defer = int(self.defer)
-        d.fuse = int(self.fuse)
-        d.keep_grads = int(self.keep_grads)
         self._applied.add(id(flat))
         return d
 

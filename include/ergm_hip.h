@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 8
+#define ERGM_ABI_VERSION 9
 
 typedef enum {
     ERGM_OK = 0,
@@ -104,24 +104,6 @@ typedef enum {
     ERGM_EPI_ACCUM = 5,
 } ergm_epilogue;
 
-/* torch.optim.AdamW applied to a weight gradient inside the epilogue of the GEMM that produces it (ABI 8):
- * for every output element C[m][n] = g (the gradient, after alpha), the parameter param[m·ldc + n] and its
- * moments exp_avg / exp_avg_sq at the same index take ergm_adamw_step's update from g (same arithmetic, bit for
- * bit), the bf16 shadow param_bf16[m·ldc + n] (optional) gets bf16 of the new parameter, and C itself is
- * written only when write_grad != 0.  Replaces the separate optimizer pass over a Conv1D weight (src/main.py:155)
- * whose gradient the GEMM has just formed (src/main.py:154): the fp32 gradient is not written and re-read.    */
-typedef struct {
-    float* param;             /* fp32 parameters aligned with C */
-    float* exp_avg;
-    float* exp_avg_sq;
-    void* param_bf16;         /* bf16 shadow aligned with C, or NULL */
-    int write_grad;           /* 1: also store the gradient into C */
-    double lr, beta1, beta2, weight_decay;
-    float eps;
-    float step_size;          /* lr / (1 - beta1^t) */
-    float bc2_sqrt;           /* sqrt(1 - beta2^t) */
-} ergm_adamw_epilogue;
-
 typedef struct {
     int M, N, K;
     int lda, ldb, ldc;
@@ -142,8 +124,6 @@ typedef struct {
                           * also write alpha·Σ_k B[k][n] (the Conv1D bias gradient, column sums of dY over
                           * the K tokens) to bias_grad[n], f32 [N]; NULL = none.  Computed from the B
                           * fragments the GEMM already stages (no second pass over dY), deterministic. */
-    const ergm_adamw_epilogue* adamw;  /* a_layout KM + b_layout KN, epilogue NONE, f32 C, bias_grad NULL only:
-                          * the AdamW update of the parameters whose gradient C is (above); NULL = none */
 } ergm_gemm_desc;
 
 /* Tuning hook (calling thread only): force pipelined-kernel configuration `cfg` (tile / wave grid /
@@ -471,14 +451,6 @@ typedef struct {
                                * waits for each block's update before that block (so they overlap the
                                * latency-bound forward instead of the throughput-bound backward); anything else
                                * that reads the parameters first calls ergm_model_optimizer_join */
-    int fuse;                 /* 1 (needs defer = 0 and every Conv1D bias stored right after its weight): every
-                               * block's six Conv1D weights + biases are updated in the epilogue of the weight-
-                               * gradient GEMM that forms their gradient (ergm_adamw_epilogue) and every LayerNorm's
-                               * γ / β in the reduction that forms theirs, instead of by the per-range passes; the
-                               * data-gradient GEMM that reads a weight's bf16 shadow runs before its update (the
-                               * stage forks the weight-gradient pair after it).  Same arithmetic, same results. */
-    int keep_grads;           /* with fuse: 1 = the fused gradients are still written to `grad`; 0 = they are not
-                               * materialised (grad holds stale values for those ranges after the backward) */
 } ergm_adamw_desc;
 int ergm_model_set_optimizer(ergm_model_plan* plan, const ergm_adamw_desc* opt);
 /* Make `stream` wait for every deferred update still pending (no-op when none). */

@@ -6,6 +6,9 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+HERE = os.path.dirname(os.path.abspath(__file__))  # test helpers (_bitwise)
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
 
 
 def pytest_configure(config):

@@ -14,6 +14,7 @@ from ergm_amd.config import ERGMConfig, NO_DROPOUT
 from ergm_amd.model import GPT2LMHeadModel
 from ergm_amd.optim import FusedAdamW
 from oracle import gpt2_oracle as O
+from _bitwise import assert_bitwise
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -187,9 +188,10 @@ def test_overlapped_adamw_matches_step_adamw(gpu, name, fp8):
         st = opt.state[model.flat]
         runs.append((model.flat.detach().clone(), model.flat_b16.clone(), st["exp_avg"].clone(),
                      st["exp_avg_sq"].clone(), evals[0], float(st["step"]), out.loss.item()))
-    for b in runs[1:]:
-        for x, y in zip(runs[0][:5], b[:5]):
-            assert torch.equal(x, y)
+    names = ("master", "shadow", "exp_avg", "exp_avg_sq", "eval logits")
+    for i, b in enumerate(runs[1:]):
+        for n, x, y in zip(names, runs[0][:5], b[:5]):
+            assert_bitwise(y, x, f"run {i + 1} {n}", model.layout)
         assert runs[0][5] == b[5] == 3.0 and runs[0][6] == b[6]
 
 
@@ -211,8 +213,8 @@ def test_compact_lookup_path_matches_dense(gpu, overlap):
             opt.step()
         torch.cuda.synchronize()
         runs.append((g, model.flat.detach().clone(), model.flat_b16.clone()))
-    for x, y in zip(*runs):
-        assert torch.equal(x, y)
+    for n, x, y in zip(("grad", "master", "shadow"), *runs):
+        assert_bitwise(y, x, f"compact {n}", model.layout)
 
 
 def test_backward_is_deterministic(gpu):
@@ -221,7 +223,7 @@ def test_backward_is_deterministic(gpu):
     _run(model, batch, gpu)
     g1 = model.flat.grad.clone()
     out = _run(model, batch, gpu)
-    assert torch.equal(g1, model.flat.grad)
+    assert_bitwise(model.flat.grad, g1, "second backward grad", model.layout)
     # gradient accumulation when the caller does not zero the gradient
     kw = {k: v.to(gpu) for k, v in batch.items()}
     out = model(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
@@ -475,7 +477,8 @@ def test_backward_chains_are_bitwise_the_single_chain(gpu, monkeypatch, B, S):
         batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=52, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
         out = _run(model, batch, gpu)
         res.append((out.loss.detach().clone(), model.flat.grad.clone()))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert_bitwise(res[1][0], res[0][0], "loss")
+    assert_bitwise(res[1][1], res[0][1], "grad", model.layout)
 
 
 @pytest.mark.parametrize("B,S", [(16, 128), (3, 32)])
@@ -492,7 +495,8 @@ def test_grouped_weight_gradient_launches_are_bitwise_the_separate_ones(gpu, mon
         batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=62, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
         out = _run(model, batch, gpu)
         res.append((out.loss.detach().clone(), model.flat.grad.clone()))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert_bitwise(res[1][0], res[0][0], "loss")
+    assert_bitwise(res[1][1], res[0][1], "grad", model.layout)
 
 
 @pytest.mark.parametrize("B,S,E,drop", [(16, 128, 128, True), (3, 37, 128, True), (2, 64, 256, False), (1, 2, 128, True),
@@ -517,8 +521,8 @@ def test_fused_attention_backward_is_bitwise_the_two_launches(gpu, monkeypatch, 
                                 sp2=V - 1, eos=V - 4)
         out = _run(model, batch, gpu)
         res.append((out.loss.detach().clone(), model.flat.grad.clone()))
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
+    assert_bitwise(res[1][0], res[0][0], "loss")
+    assert_bitwise(res[1][1], res[0][1], "grad", model.layout)
 
 
 @pytest.mark.parametrize("B,S,E,drop", [(16, 128, 128, True), (3, 37, 128, True), (2, 64, 256, False), (1, 2, 128, True),
@@ -542,48 +546,48 @@ def test_fused_cross_attention_forward_is_bitwise_the_two_launches(gpu, monkeypa
                                 sp2=V - 1, eos=V - 4)
         out = _run(model, batch, gpu)
         res.append((out.loss.detach().clone(), out.logits_bf16.clone(), model.flat.grad.clone()))
-    for x, y in zip(*res):
-        assert torch.equal(x, y)
+    for n, x, y in zip(("loss", "logits", "grad"), *res):
+        assert_bitwise(y, x, n, model.layout)
 
 
 @pytest.mark.parametrize("B,S,E", [(16, 128, 128), (3, 37, 128), (2, 64, 256)])
-def test_fused_optimizer_is_bitwise_the_per_range_update(gpu, B, S, E):
-    """FusedAdamW(fuse=True): every block's Conv1D weights + biases updated in the epilogue of the weight-gradient
-    GEMM that forms their gradient and the LayerNorm parameters in their gradient reduction (the weight-gradient
-    pairs forked after the data-gradient GEMM that last reads the bf16 shadow) give bitwise the parameters, moments,
-    bf16 shadow and losses of the per-range passes over three steps with dropout and a scheduled LR; with
-    keep_grads the gradients too.  B = 16, S = 128 is C2's token count (grouped pipelined launches), B = 3, S = 37
-    an odd token count (register-staged kernels, scalar epilogue)."""
+def test_executor_scheduled_optimizer_is_bitwise_the_step_update(gpu, B, S, E):
+    """FusedAdamW(overlap=True): the executor launches each bucket's AdamW on its optimizer stream during the
+    backward, ordered only by the side stream's stage marks (ergm_model_set_optimizer, opt_wait) — bitwise the
+    parameters, moments, bf16 shadow, gradients and losses of the plain step() after the backward, at every step of
+    three with dropout and a scheduled LR.  B = 16, S = 128 is C2's token count (grouped pipelined launches), B = 3,
+    S = 37 an odd one (register-staged kernels), (2, 64, 256) the shape of the round-4 fused-optimizer mismatch.  A
+    failure names the step, the buffer and the parameter of the first differing element (tests/_bitwise.py)."""
     from ergm_amd.data import synthetic_batch
     from ergm_amd.optim import get_polynomial_decay_schedule_with_warmup
     V = 512
     runs = []
-    for fuse, keep in ((False, True), (True, True), (True, False)):
+    for overlap in (False, True):
         torch.manual_seed(7)
         cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64, n_positions=1024)
         model = GPT2LMHeadModel(cfg, device=gpu)
         model.load_state_dict(O.init_params(O.OracleConfig(vocab_size=V, n_embd=E, n_layer=2, n_head=E // 64,
                                                            n_positions=1024), seed=71), strict=False)
         batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=72, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
-        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=True, fuse=fuse, keep_grads=keep)
+        opt = FusedAdamW([model.flat], lr=1e-3, model=model, overlap=overlap)
         sched = get_polynomial_decay_schedule_with_warmup(opt, 1, 10, power=2.0)
-        losses = []
+        steps = []
         for _ in range(3):
             opt.zero_grad()
             out = _run(model, batch, gpu)
             g = model.flat.grad.clone()
             opt.step()
             sched.step()
-            losses.append(out.loss.item())
-        torch.cuda.synchronize()
-        st = opt.state[model.flat]
-        runs.append((model.flat.detach().clone(), model.flat_b16.clone(), st["exp_avg"].clone(),
-                     st["exp_avg_sq"].clone(), losses, g))
-    for r in runs[1:]:
-        for x, y in zip(runs[0][:4], r[:4]):
-            assert torch.equal(x, y)
-        assert runs[0][4] == r[4]
-    assert torch.equal(runs[0][5], runs[1][5])  # keep_grads: the gradients are written too
+            torch.cuda.synchronize()
+            st = opt.state[model.flat]
+            steps.append(dict(loss=out.loss.detach().clone(), grad=g, master=model.flat.detach().clone(),
+                              shadow=model.flat_b16.clone(), exp_avg=st["exp_avg"].clone(),
+                              exp_avg_sq=st["exp_avg_sq"].clone()))
+        runs.append((model.layout, steps))
+    lay = runs[0][0]
+    for k, (ref, got) in enumerate(zip(runs[0][1], runs[1][1])):
+        for name in ("loss", "grad", "master", "shadow", "exp_avg", "exp_avg_sq"):
+            assert_bitwise(got[name], ref[name], f"step {k + 1} {name} (overlapped vs step())", lay)
 
 
 def test_device_train_metrics_match_framework_ops(gpu):
@@ -640,7 +644,7 @@ def test_custom_op_registration_and_torch_compile(gpu):
         torch.cuda.synchronize()
         outs.append((out.loss.detach().clone(), out.logits.detach().clone(), model.flat.grad.clone()))
     for a, b in zip(*outs):
-        assert torch.equal(a, b)
+        assert_bitwise(b, a, "compiled vs eager", model.layout)
 
 
 def test_compiled_logits_gradient_opt_in(gpu):

@@ -119,50 +119,6 @@ def test_gemm_bias_grad(gpu, M, N, K, split, cfg):
         ops.gemm(X.t().contiguous(), dY, M, N, K, a_layout=L.MK, b_layout=L.KN, bias_grad=db)
 
 
-@pytest.mark.parametrize("M,N,K,split,cfg", [(769, 2304, 2048, 1, -1), (3073, 768, 2048, 1, -1),
-                                               (200, 136, 1000, 1, -1), (257, 512, 2048, 3, -1),
-                                               (257, 512, 1024, 1, 0), (257, 512, 1024, 1, 10),
-                                               (257, 512, 1024, 1, 16), (257, 512, 1024, 1, 33)])
-def test_gemm_adamw_epilogue_is_bitwise_the_separate_update(gpu, M, N, K, split, cfg):
-    """ergm_adamw_epilogue: a weight-gradient GEMM (KM x KN, f32 out) that applies torch AdamW to the parameters laid
-    out like its output gives bitwise the parameters, moments and bf16 shadow of the same GEMM followed by
-    ergm_adamw_step, over every epilogue path (the staged pipelined epilogue with batched parameter loads, its 8-wave
-    and warp-specialised / KS2 variants, split-K's reduce, the register-staged kernel's scalar epilogue for
-    K % 64 != 0); with write_grad the gradient is written as well, without it C is left untouched."""
-    g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    ld = (M + 7) // 8 * 8  # the executor's activations carry a ones column and padding (row stride E + 8)
-    X = (torch.randn(K, ld, generator=g) * 0.5).to(gpu, torch.bfloat16)[:, :M]  # [tokens][in+1]  (KM)
-    dY = (torch.randn(K, N, generator=g) * 0.5).to(gpu, torch.bfloat16)        # [tokens][out]   (KN)
-    p0 = torch.randn(M, N, generator=g).to(gpu)
-    m0 = (0.01 * torch.randn(M, N, generator=g)).to(gpu)
-    v0 = (0.01 * torch.rand(M, N, generator=g)).to(gpu)
-    hp = dict(lr=3e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, step=3)
-    L.check(L.load().ergm_gemm_tune(cfg, split if cfg >= 0 else 0), "tune")
-    try:
-        # reference: the gradient, then the separate optimizer pass
-        gW = ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, split_k=split if cfg < 0 else 0)
-        p1, m1, v1 = p0.clone(), m0.clone(), v0.clone()
-        s1 = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-        ops.adamw_step(p1, gW, m1, v1, s1, hp["lr"], 0.9, 0.999, 1e-8, 0.01, hp["step"])
-        res = []
-        for wg in (True, False):
-            p2, m2, v2 = p0.clone(), m0.clone(), v0.clone()
-            s2 = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-            C2 = torch.full((M, N), 7.0, device=gpu)
-            ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, split_k=split if cfg < 0 else 0, out=C2,
-                     adamw=dict(hp, param=p2, exp_avg=m2, exp_avg_sq=v2, shadow=s2, write_grad=wg))
-            res.append((p2, m2, v2, s2, C2))
-    finally:
-        L.load().ergm_gemm_tune(-1, 0)
-    torch.cuda.synchronize()
-    for i, (p2, m2, v2, s2, C2) in enumerate(res):
-        assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2) and torch.equal(s1, s2)
-        assert torch.equal(C2, gW) if i == 0 else bool((C2 == 7.0).all())
-    with pytest.raises(ValueError):  # other layouts reject it
-        ops.gemm(X.t().contiguous(), dY, M, N, K, a_layout=L.MK, b_layout=L.KN, out=C2,
-                 adamw=dict(hp, param=p2, exp_avg=m2, exp_avg_sq=v2))
-
-
 def test_gemm_epilogues(gpu):
     M, N, K = 256, 384, 192
     A = torch.randn(M, K, device=gpu).bfloat16()
