@@ -105,9 +105,12 @@ def compare(tag, a, b, rtol):
 
 
 def build_case(refmodel, name, cfg, B, S, seed, with_features=True, visual_rows=1, n_turns=5,
-               full_grads=True, vocab_hi=None):
-    print(f"[{name}] L={cfg.n_layer} E={cfg.n_embd} H={cfg.n_head} V={cfg.vocab_size} B={B} S={S}")
+               full_grads=True, vocab_hi=None, xpeak=None):
+    print(f"[{name}] L={cfg.n_layer} E={cfg.n_embd} H={cfg.n_head} V={cfg.vocab_size} B={B} S={S}"
+          + (f" cross-attention gains {xpeak}" if xpeak else ""))
     P = O.init_params(cfg, seed=seed)
+    if xpeak:  # peaked cross-attention (oracle.peak_cross_attention): every gradient at the model's scale
+        O.peak_cross_attention(P, cfg.n_layer, *xpeak)
     vhi = vocab_hi if vocab_hi is not None else cfg.vocab_size - 3
     batch = synthetic_batch(B, S, n_turns=n_turns, feat_dim=cfg.n_embd, seed=seed + 1000,
                             vocab_hi=vhi, visual_rows=visual_rows, with_features=with_features,
@@ -125,6 +128,7 @@ def build_case(refmodel, name, cfg, B, S, seed, with_features=True, visual_rows=
         "config": np.array([cfg.vocab_size, cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_positions],
                            dtype=np.int64),
         "seed": np.array(seed),
+        **({"xpeak_gains": np.array(xpeak, dtype=np.float64)} if xpeak else {}),
         "loss": ref_out.loss.detach().numpy(),
         "loss_lm": ora_out["loss_lm"].numpy(),
         "loss_emotion": ora_out["loss_emotion"].numpy(),
@@ -432,6 +436,25 @@ def optim_case(refmodel):
     return rec
 
 
+XPEAK_E128 = (50.0, 50.0, 10.0)   # cross-attention scores std 2.5, mean max softmax probability 0.45 (vs 1/32 flat)
+XPEAK_C2 = (20.0, 20.0, 10.0)     # GPT-2-small: scores std 2.4, mean max probability 0.32 (vs 1/128 flat)
+
+
+def xpeak_case(refmodel, name):
+    """Peaked cross-attention: the reference's gradients with the caption-side projections
+    scaled so the cross-attention softmax is far from uniform — no gradient is tiny against the model's scale, so
+    the GPU gate holds every tensor, query side included, to the relative bound.  Two heads, full gradients at
+    E = 128; norms and heads at the GPT-2-small C2 slice (12 heads, 12 blocks)."""
+    if name == "xpeak_e128":
+        cfg = O.OracleConfig(vocab_size=256, n_embd=128, n_layer=2, n_head=2, n_positions=64)
+        _, _, rec = build_case(refmodel, name, cfg, B=2, S=32, seed=66, xpeak=XPEAK_E128)
+    else:
+        cfg = O.OracleConfig()
+        _, _, rec = build_case(refmodel, name, cfg, B=2, S=128, seed=77, full_grads=False, vocab_hi=50257,
+                               xpeak=XPEAK_C2)
+    return rec
+
+
 def main():
     torch.manual_seed(0)
     refmodel = load_reference()
@@ -441,7 +464,9 @@ def main():
         cases = {"imgs2d": ("imgs2d_e64.npz", lambda: imgs2d_case(refmodel)),
                  "dataset": ("dataset_ref.npz", dataset_case),
                  "trainer": ("trainer_ref.npz", lambda: trainer_case(refmodel)),
-                 "optim": ("optim_ref.npz", lambda: optim_case(refmodel))}
+                 "optim": ("optim_ref.npz", lambda: optim_case(refmodel)),
+                 "xpeak": ("xpeak_e128.npz", lambda: xpeak_case(refmodel, "xpeak_e128")),
+                 "xpeak_c2": ("xpeak_c2slice.npz", lambda: xpeak_case(refmodel, "xpeak_c2slice"))}
         for c in only:
             fn, make = cases[c]
             np.savez_compressed(os.path.join(out_dir, fn), **make())

@@ -36,6 +36,8 @@ def _setup(rec, gpu):
     ocfg = O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P)
     cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P, **NO_DROPOUT)
     P0 = O.init_params(ocfg, seed=int(rec["seed"]))
+    if "xpeak_gains" in rec:  # peaked cross-attention fixtures (tests/golden/make_golden.py xpeak_case)
+        O.peak_cross_attention(P0, Lyr, *(float(x) for x in rec["xpeak_gains"]))
     model = GPT2LMHeadModel(cfg, device=gpu)
     model.load_state_dict(P0, strict=False)
     batch = {k[3:]: torch.from_numpy(v) for k, v in rec.items() if k.startswith("in_")}
@@ -124,6 +126,58 @@ def test_gpt2_small_matches_reference_and_oracle(gpu, name):
     for k in g:  # the oracle's gradients are the reference's (golden norms)
         ref = float(rec["gradnorm:" + k])
         assert abs(og[k].double().norm().item() - ref) <= 1e-4 * ref + 1e-12, k
+
+
+def _strict_grad_gate(got: dict, ref: dict, rtol=GRAD_RTOL):
+    """Every tensor within rel-L2 rtol of its reference — no absolute floor — and, so that the case is the one it
+    claims to be, none of them small enough for _grad_gate's floor to have applied."""
+    rms = max(torch.as_tensor(v).double().norm().item() / max(torch.as_tensor(v).numel(), 1) ** 0.5
+              for v in ref.values())
+    floored = [k for k, r in ref.items()
+               if torch.as_tensor(r).double().norm().item() < 1e-3 * rms * torch.as_tensor(r).numel() ** 0.5]
+    assert not floored, f"tensors under the absolute floor: {floored}"
+    bad = [(k, round(_rel(got[k], r), 4)) for k, r in ref.items() if _rel(got[k], r) > rtol]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("attn_fuse,xq_fuse", [("1", "1"), ("0", "0")])
+def test_peaked_cross_attention_matches_reference_every_gradient(gpu, monkeypatch, attn_fuse, xq_fuse):
+    """Cross-attention far from uniform (under the N(0, 0.02) init its softmax is flat and the
+    query-side gradients passed only through _grad_gate's absolute floor).  xpeak_e128.npz is the reference's own
+    forward + backward with the caption-side projections scaled (scores std 2.5, mean max probability 0.45; two
+    heads): loss, logits and EVERY gradient — crossattention.q_attn, crossattention.c_attn and ln_cross_attn
+    included — within the relative gates, no floor, through the fused kernels (attn_fwd_qgemm, attn_bwd_fused) and
+    the separate launches (ERGM_XQ_FUSE=0, ERGM_ATTN_FUSE=0)."""
+    monkeypatch.setenv("ERGM_ATTN_FUSE", attn_fuse)
+    monkeypatch.setenv("ERGM_XQ_FUSE", xq_fuse)
+    rec = _load("xpeak_e128.npz")
+    ocfg, cfg, P0, model, batch = _setup(rec, gpu)
+    out = _run(model, batch, gpu)
+    ref_loss = float(rec["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    assert (out.logits.float().cpu() - torch.from_numpy(rec["logits"])).abs().max().item() <= LOGIT_ATOL
+    _emotion_gate(out.emotion_logits, rec["emotion_logits"])
+    g = _grads(model)
+    _strict_grad_gate(g, {k: rec["grad:" + k] for k in g})
+
+
+def test_peaked_cross_attention_gpt2_small_every_gradient(gpu):
+    """The same at the GPT-2-small C2 slice (12 blocks, 12 heads, B = 2, S = 128): the reference's gradient norms
+    pin the oracle (xpeak_c2slice.npz), the oracle's full gradients hold every HIP gradient to the relative gate
+    (no floor), the loss and logits slices to the reference's."""
+    rec = _load("xpeak_c2slice.npz")
+    ocfg, cfg, P0, model, batch = _setup(rec, gpu)
+    out = _run(model, batch, gpu)
+    ref_loss = float(rec["loss"])
+    assert abs(out.loss.item() - ref_loss) <= LOSS_RTOL * abs(ref_loss)
+    lg = out.logits.float().cpu()
+    assert (lg[:, :4, :64] - torch.from_numpy(rec["logits_head"])).abs().max().item() <= LOGIT_ATOL
+    assert (lg[:, -2:, -64:] - torch.from_numpy(rec["logits_tail"])).abs().max().item() <= LOGIT_ATOL
+    _, og = O.loss_and_grads(P0, ocfg, batch)
+    for k, v in og.items():
+        ref = float(rec["gradnorm:" + k])
+        assert abs(v.double().norm().item() - ref) <= 1e-4 * ref + 1e-12, k
+    _strict_grad_gate(_grads(model), og)
 
 
 def test_adamw_step_and_loss_decrease(gpu):

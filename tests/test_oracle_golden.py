@@ -32,16 +32,24 @@ def _cfg(rec):
     return O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=H, n_positions=P)
 
 
+def _params(rec, cfg):
+    """The fixture's weights: the oracle's seeded init, with the peaked cross-attention gains when recorded."""
+    P = O.init_params(cfg, seed=int(rec["seed"]))
+    if "xpeak_gains" in rec:
+        O.peak_cross_attention(P, cfg.n_layer, *(float(x) for x in rec["xpeak_gains"]))
+    return P
+
+
 def _rel(a, b):
     a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("name", ["tiny_e64.npz", "small_e128_v500.npz"])
+@pytest.mark.parametrize("name", ["tiny_e64.npz", "small_e128_v500.npz", "xpeak_e128.npz"])
 def test_oracle_matches_reference_small(name):
     rec = _load(name)
     cfg = _cfg(rec)
-    P = O.init_params(cfg, seed=int(rec["seed"]))
+    P = _params(rec, cfg)
     out, grads = O.loss_and_grads(P, cfg, _batch(rec))
     assert abs(out["loss"].item() - float(rec["loss"])) <= 1e-5 * abs(float(rec["loss"]))
     assert _rel(out["emotion_logits"], rec["emotion_logits"]) < 1e-5
@@ -55,11 +63,11 @@ def test_oracle_matches_reference_small(name):
             assert _rel(g.reshape(-1)[:32], rec["gradhead:" + k]) < 1e-3, k
 
 
-@pytest.mark.parametrize("name", ["c1_gpt2small_textonly.npz", "c2slice_gpt2small_fusion.npz"])
+@pytest.mark.parametrize("name", ["c1_gpt2small_textonly.npz", "c2slice_gpt2small_fusion.npz", "xpeak_c2slice.npz"])
 def test_oracle_matches_reference_gpt2_small(name):
     rec = _load(name)
     cfg = _cfg(rec)
-    P = O.init_params(cfg, seed=int(rec["seed"]))
+    P = _params(rec, cfg)
     out, grads = O.loss_and_grads(P, cfg, _batch(rec))
     assert abs(out["loss"].item() - float(rec["loss"])) <= 1e-5 * abs(float(rec["loss"]))
     assert _rel(out["emotion_logits"], rec["emotion_logits"]) < 1e-5
