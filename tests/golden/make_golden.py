@@ -437,7 +437,10 @@ def optim_case(refmodel):
 
 
 XPEAK_E128 = (50.0, 50.0, 10.0)   # cross-attention scores std 2.5, mean max softmax probability 0.45 (vs 1/32 flat)
-XPEAK_C2 = (20.0, 20.0, 10.0)     # GPT-2-small: scores std 2.4, mean max probability 0.32 (vs 1/128 flat)
+# GPT-2-small: scores std 1.4, mean max probability 0.12 (vs 1/128 flat).  Stronger gains amplify bf16 rounding
+# through the 12 blocks beyond the bf16 gates for the reference itself: at (20, 20, 10) the reference under CPU bf16
+# autocast deviates from its fp32 gradients by up to 6.9 % (rel-L2), at (15, 15, 5) by 1.8 %.
+XPEAK_C2 = (15.0, 15.0, 5.0)
 
 
 def xpeak_case(refmodel, name):

@@ -165,7 +165,9 @@ def test_peaked_cross_attention_gpt2_small_every_gradient(gpu):
     """The same at the GPT-2-small C2 slice (12 blocks, 12 heads, B = 2, S = 128): the reference's gradient norms
     pin the oracle (xpeak_c2slice.npz), the oracle's full gradients hold every HIP gradient to the relative gate
     (no floor: the last blocks' cross-attention gradients are 3x below where _grad_gate's floor would start at this
-    depth, and are held to rel-L2 3e-2 regardless), the loss and logits slices to the reference's."""
+    depth, and are held to rel-L2 3e-2 regardless), the loss and logits slices to the reference's.  Scores std 1.4,
+    mean max probability 0.12 against 1/128 flat; the reference's own bf16-autocast deviation at these gains is 1.8 %
+    (stronger gains push it past the gate for the reference itself: make_golden.py XPEAK_C2)."""
     rec = _load("xpeak_c2slice.npz")
     ocfg, cfg, P0, model, batch = _setup(rec, gpu)
     out = _run(model, batch, gpu)
