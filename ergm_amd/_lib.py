@@ -37,8 +37,7 @@ class GemmDesc(C.Structure):
                 ("ldc", C.c_int), ("a_layout", C.c_int), ("b_layout", C.c_int), ("c_dtype", C.c_int),
                 ("epilogue", C.c_int), ("alpha", C.c_float), ("bias", C.c_void_p), ("aux", C.c_void_p),
                 ("ld_aux", C.c_int), ("aux_out", C.c_void_p), ("ld_aux_out", C.c_int), ("split_k", C.c_int),
-                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p),
-                ("bias_part", C.c_void_p)]
+                ("alpha_dev", C.c_void_p), ("dropout", C.POINTER(Dropout)), ("bias_grad", C.c_void_p)]
 
 
 class AdamWDesc(C.Structure):
@@ -78,7 +77,6 @@ _SIGS = {
     "ergm_gemm_trace": (i32, [i32, vp, i32]),
     "ergm_gemm_workspace_size": (sz, [C.POINTER(GemmDesc)]),
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
-    "ergm_gemm_bias_rows": (i32, [C.POINTER(GemmDesc)]),
     "ergm_gemm_f8": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, vp, vp]),
     "ergm_gemm_f8_tune": (i32, [i32]),
     "ergm_quant_rows_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp]),

@@ -46,8 +46,6 @@ struct GemmArgs {
     DropSite drop;         // BIAS_RESID: dropout of the residual branch (src/model.py:245,266), rows m, cols n
     float* colsum;         // KM x KN, EPI_NONE: bias gradient alpha·Σ_k B[k][n] -> colsum[n] (nullptr: none)
     float* colsum_part;    // split-K: per-split partial column sums [z][N] (combined by splitk_reduce_kernel)
-    int cs_rows;           // 1 (ergm_gemm_desc.bias_part): EVERY tile row tm sums its share of the K steps,
-                           // [tm·nk/tiles_m, (tm+1)·nk/tiles_m), into colsum[tm·N + n] (unsplit launches only)
     int xcd_split;         // split-K over 8 K slices, one per XCD: grid.x = 8·tiles, slice = blockIdx.x & 7, so
                            // every tile of one K slice shares an XCD's L2 (pipelined kernel only)
     // MX-fp8 GEMM (gemm_mx_kernel): e8m0 scales of every 32-element K block, A [M][ld_sa], B [N][ld_sb] bytes
@@ -415,12 +413,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     // weight-gradient bias: the waves of the last tile row with wm == 0 also sum the B (dY) fragments they
     // read: lane l holds B[k = 8(l>>4) .. +7][n = l & 15] of each 16-column fragment
     constexpr bool CS = A_KM && B_KN && EPI == ERGM_EPI_NONE && !OUT_BF16;
-    // cs_rows: the wm == 0 waves of every tile row sum a 1/tiles_m share of the K steps (the bias row of an augmented
-    // [K+1]-row weight gradient would be a whole extra tile row of 1 useful row; one row summing all K steps is the
-    // long pole at T = 4096)
-    const bool do_cs = CS && a.colsum && wm == 0 && (a.cs_rows || tm == a.tiles_m - 1);
-    const int cs_lo = a.cs_rows ? tm * nk / a.tiles_m : 0;
-    const int cs_hi = a.cs_rows ? (tm + 1) * nk / a.tiles_m : nk;
+    const bool do_cs = CS && a.colsum && tm == a.tiles_m - 1 && wm == 0;
     float cs[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) cs[j] = 0.f;
@@ -452,7 +445,6 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
                     }
                 }
                 if constexpr (SUM) {  // packed bf16 dot products against ones: 4 v_dot2 per fragment
-                  if (kt >= cs_lo && kt < cs_hi) {
                     const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
 #pragma unroll
                     for (int j = 0; j < FN; ++j) {
@@ -463,7 +455,6 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
                         t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(fb[j], fb[j], 6, 7), one, t, false);
                         cs[j] = t;
                     }
-                  }
                 }
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
@@ -488,7 +479,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     if constexpr (CS) {
         if (do_cs) {  // sum the four 16-lane rows (k groups), lane position (column) preserved
             const int lane = threadIdx.x & 63;
-            float* dst = a.cs_rows ? a.colsum + (size_t)tm * a.N : a.slab ? a.colsum_part + (size_t)zs * a.N : a.colsum;
+            float* dst = a.slab ? a.colsum_part + (size_t)zs * a.N : a.colsum;
             const float sc = a.slab ? 1.0f : alpha;  // split-K: the reduce kernel applies alpha
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
@@ -1564,11 +1555,6 @@ extern "C" int ergm_gemm_trace(int on, int* shapes, int max_shapes) {
 }
 
 namespace ergm {
-// Plans whose pipelined kernel can write per-tile-row bias partials (ergm_gemm_desc.bias_part): the staged (non-warp-
-// specialised, single-group) body, unsplit.
-static bool bias_rows_ok(const GemmPlan& p) {
-    return p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 && p.split == 1 && !p.xcd;
-}
 // Kernel arguments of one planned GEMM (split-K slabs are set by the caller).
 static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B, void* C, const GemmPlan& p) {
     GemmArgs a;
@@ -1597,11 +1583,6 @@ static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B,
     const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1;
     a.colsum = cs_in ? d->bias_grad : nullptr;
     a.colsum_part = nullptr;
-    a.cs_rows = 0;
-    if (d->bias_part && bias_rows_ok(p)) {
-        a.colsum = d->bias_part;
-        a.cs_rows = 1;
-    }
     a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 ? 1 : 0;
     return a;
 }
@@ -1639,22 +1620,10 @@ static int validate_desc(const ergm_gemm_desc* d, const void* A, const void* B, 
     ERGM_CHECK_ARG(!d->bias_grad || (d->a_layout == ERGM_KM && d->b_layout == ERGM_KN && e == ERGM_EPI_NONE &&
                                      d->c_dtype == ERGM_F32),
                    "ergm_gemm: bias_grad needs a_layout KM, b_layout KN, epilogue NONE and f32 C");
-    ERGM_CHECK_ARG(!d->bias_part || (d->a_layout == ERGM_KM && d->b_layout == ERGM_KN && e == ERGM_EPI_NONE &&
-                                     d->c_dtype == ERGM_F32 && !d->bias_grad),
-                   "ergm_gemm: bias_part needs a_layout KM, b_layout KN, epilogue NONE, f32 C and no bias_grad");
 
     return ERGM_OK;
 }
 }  // namespace ergm
-
-extern "C" int ergm_gemm_bias_rows(const ergm_gemm_desc* d) {
-    if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->a_layout != ERGM_KM || d->b_layout != ERGM_KN ||
-        d->epilogue != ERGM_EPI_NONE || d->c_dtype != ERGM_F32)
-        return 0;
-    if (!pipe_ok(d)) return 0;
-    const GemmPlan p = plan_gemm(d);
-    return bias_rows_ok(p) ? cdiv(d->M, p.bm) : 0;
-}
 
 extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, void* C, void* ws,
                          size_t ws_bytes, void* stream) {
@@ -1662,8 +1631,6 @@ extern "C" int ergm_gemm(const ergm_gemm_desc* d, const void* A, const void* B, 
     const int e = d->epilogue;
     trace_shape(d);
     GemmPlan p = plan_gemm(d);
-    ERGM_CHECK_ARG(!d->bias_part || bias_rows_ok(p),
-                   "ergm_gemm: bias_part: this shape's plan has no per-tile-row column sums (ergm_gemm_bias_rows = 0)");
     GemmArgs a = make_args(d, A, B, C, p);
     const bool cs_in = a.colsum != nullptr;
     hipStream_t s = as_stream(stream);

@@ -53,8 +53,7 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
-                             float* const* dgamma, float* const* dbeta, hipStream_t s, int nb, const float* const* bpart,
-                             const int* brows, const int* bcols, float* const* bout);
+                             float* const* dgamma, float* const* dbeta, hipStream_t s);
 int loss_finalize_metrics(const float* row_loss, int T, const int* n_valid_global, const float* emo_loss_sum,
                           const int* n_valid_emo, float* out, float* loss_acc, int64_t* correct,
                           const float* emo_logits, const int64_t* emo_labels, int B, int C, hipStream_t s);
@@ -110,16 +109,6 @@ struct ergm_model_plan {
     // dW GEMM over K+1 rows also yields the bias gradient (each bias is stored right after its weight).
     int XE, XF;
     bool fused_bias;  // the ones-column layout holds (every bias right after its weight): dW over M+1 rows
-    // per-tile-row bias partials (ergm_gemm_desc.bias_part): the weight-gradient GEMMs of a stage write their bias
-    // gradient as [rows][N] partial column sums into these slabs (one per dW GEMM of a block, + the caption K/V),
-    // reduced in row order by the stage's LayerNorm parameter reduce (ERGM_BIAS_ROWS=0: the augmented ones row)
-    bool bias_rows;
-    float* bias_slab[7];
-    int bias_k;                // next slab of the stage
-    int bias_pending;          // pending bias reductions (slab, rows, cols, out)
-    const float* bp_part[8];
-    int bp_rows[8], bp_cols[8];
-    float* bp_out[8];
     // activations
     float** resid;  // 3L+1 residual-stream tensors [T][E] f32
     std::vector<float*> resid_v;
@@ -199,6 +188,9 @@ struct ergm_model_plan {
     // (and the stacked caption K/V GEMM in forward), forked/joined with events.
     hipStream_t side;
     hipEvent_t ev_fork;  // fork points are bound to the producing launch (common.h ERGM_LAUNCH) or recorded
+    // the stage's final fork point from the caller's stream (ln_reduce_flush), valid until the native call that took
+    // it returns: the optimizer updates launched behind the stage wait on it (opt_wait) instead of a new marker
+    hipEvent_t stage_pt = nullptr;
     std::vector<hipEvent_t> ev_join;  // one per backward stage (L layers + head + embed)
     // inputs
     const int64_t *ids, *tt, *cap_ids, *labels, *emo_labels;
@@ -345,11 +337,6 @@ size_t carve(ergm_model_plan* P, char* base) {
     for (size_t i = 0; i < 3 * L + 1; ++i) P->dhb[i] = c.take<__bf16>(T * E);
     P->ln_part.assign(3 * L + 1, nullptr);
     for (size_t i = 0; i < 3 * L + 1; ++i) P->ln_part[i] = c.take<float>((size_t)2 * ln_bwd_nparts((int)T) * E);
-    {  // bias slabs: cdiv(M, 64) rows (the smallest tile) x N for the block's six weight gradients and the caption K/V
-        const size_t r1 = (size_t)(E + 63) / 64, rF = (size_t)(F + 63) / 64;
-        const size_t cnt[7] = {rF * E, r1 * F, r1 * E, r1 * E, r1 * E, r1 * 3 * E, r1 * 2 * E * L};
-        for (int i = 0; i < 7; ++i) P->bias_slab[i] = c.take<float>(cnt[i]);
-    }
     P->dpre.assign(L, nullptr); P->dxq.assign(L, nullptr); P->dqkv.assign(L, nullptr);
     for (size_t l = 0; l < L; ++l) {
         P->dpre[l] = c.take<__bf16>(T * F);
@@ -545,42 +532,22 @@ struct LaunchClass {
 // sums gB from the dY fragments it stages (ergm_gemm_desc.bias_grad: measured equal at C2 but +4 % step time
 // at C4, where its last tile row carrying the column sums through 64 K steps becomes the long pole).
 double dw_flops(const ergm_model_plan* P, const DwJob& j) { return 2.0 * j.M * j.N * P->T + (double)j.N * P->T; }
-// With bias_rows the GEMM runs over the M weight rows only and writes the bias as per-tile-row partials into the
-// stage's next slab (ergm_gemm_desc.bias_part), queued for the stage's reduce (bias_reduce_add); a shape whose plan
-// cannot (ergm_gemm_bias_rows = 0) keeps the ones row / in-GEMM column sum.
-// Returns the bias rows written into slab `slab` (0: the fallback); bias_commit queues them once launched.
-int dw_desc(const ergm_model_plan* P, const DwJob& j, ergm_gemm_desc& g, int slab) {
+void dw_desc(const ergm_model_plan* P, const DwJob& j, ergm_gemm_desc& g) {
     memset(&g, 0, sizeof(g));
-    g.M = j.M;
+    g.M = P->fused_bias ? j.M + 1 : j.M;
     g.N = j.N; g.K = P->T; g.lda = j.lda; g.ldb = j.ldy; g.ldc = j.ldc;
     g.a_layout = ERGM_KM; g.b_layout = ERGM_KN; g.c_dtype = ERGM_F32; g.epilogue = ERGM_EPI_NONE;
     g.alpha = 1.0f;
-    const int rows = P->bias_rows && slab < 7 && j.ldc == j.N ? ergm_gemm_bias_rows(&g) : 0;
-    if (rows > 0) {
-        g.bias_part = P->bias_slab[slab];
-        return rows;
-    }
-    g.M = P->fused_bias ? j.M + 1 : j.M;
     g.bias_grad = P->fused_bias ? nullptr : j.gB;
-    return 0;
-}
-int bias_commit(ergm_model_plan* P, const ergm_gemm_desc& g, int rows, const DwJob& j) {
-    if (rows <= 0) return ERGM_OK;
-    ++P->bias_k;
-    if (P->dry) return ERGM_OK;
-    ERGM_CHECK_ARG(P->bias_pending < 8, "model: too many pending bias reductions");
-    const int k = P->bias_pending++;
-    P->bp_part[k] = g.bias_part; P->bp_rows[k] = rows; P->bp_cols[k] = j.N; P->bp_out[k] = j.gB;
-    return ERGM_OK;
 }
 int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
     Probe pr(P, 5, s, dw_flops(P, j));
     ergm_gemm_desc g;
-    const int rows = dw_desc(P, j, g, P->bias_k);
+    dw_desc(P, j, g);
     const size_t w = ergm_gemm_workspace_size(&g);
     ERGM_TRY(ws_need(P, w));
-    if (!P->dry) ERGM_TRY(ergm_gemm(&g, j.A, j.dY, j.gW, s == P->side ? P->scratch2 : P->scratch, P->scratch_bytes, s));
-    return bias_commit(P, g, rows, j);
+    if (P->dry) return ERGM_OK;
+    return ergm_gemm(&g, j.A, j.dY, j.gW, s == P->side ? P->scratch2 : P->scratch, P->scratch_bytes, s);
 }
 // Two pending weight-gradient GEMMs as ONE grouped launch (gemm_dw_pair) when they plan to the same unsplit
 // configuration: each alone has fewer tiles than the chip has CUs (ERGM_DW_GROUP=0: two launches).
@@ -588,19 +555,15 @@ int dw_launch(ergm_model_plan* P, hipStream_t s, const DwJob& j) {
 int dw_launch_pair(ergm_model_plan* P, hipStream_t s, const DwJob& j0, const DwJob& j1) {
     if (!P->dw_group) return ERGM_EUNSUPPORTED;
     ergm_gemm_desc g[2];
-    const int r0 = dw_desc(P, j0, g[0], P->bias_k);
-    const int r1 = dw_desc(P, j1, g[1], P->bias_k + (r0 > 0 ? 1 : 0));
+    dw_desc(P, j0, g[0]);
+    dw_desc(P, j1, g[1]);
     const ergm_gemm_desc* d[2] = {&g[0], &g[1]};
     const void* A[2] = {j0.A, j1.A};
     const void* B[2] = {j0.dY, j1.dY};
     void* C[2] = {j0.gW, j1.gW};
     ERGM_TRY(gemm_dw_pair(d, A, B, C, s, false));
-    {
-        Probe pr(P, 5, s, dw_flops(P, j0) + dw_flops(P, j1));
-        ERGM_TRY(gemm_dw_pair(d, A, B, C, s, true));
-    }
-    ERGM_TRY(bias_commit(P, g[0], r0, j0));
-    return bias_commit(P, g[1], r1, j1);
+    Probe pr(P, 5, s, dw_flops(P, j0) + dw_flops(P, j1));
+    return gemm_dw_pair(d, A, B, C, s, true);
 }
 // Queue a weight-gradient GEMM; dw_flush launches the queue on the side stream behind ONE fork from the data-
 // gradient chain(s).
@@ -661,17 +624,17 @@ int ln_bwd(ergm_model_plan* P, hipStream_t s, const float* x, const float* mean,
     return ln_reduce_add(P, slot, dgamma, dbeta);
 }
 
-// One side-stream launch per stage sums the pending LayerNorms' dγ/dβ partials and the stage's weight-gradient bias
-// partials (bias_rows), each in fixed row order.
 int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
-    P->bias_k = 0;
-    if (P->dry || (P->ln_pending == 0 && P->bias_pending == 0)) return ERGM_OK;
-    if (P->ln_pending) ERGM_TRY(fork_side(P, ch));  // the partials of the chain's LayerNorm backwards
-    const int n = P->ln_pending, nb = P->bias_pending;
+    if (P->dry || P->ln_pending == 0) return ERGM_OK;
+    {  // behind the chains' LayerNorm backwards (their partials)
+        hipEvent_t e = stream_point(P, ch.s[0], P->ev_fork);
+        if (!e || hipStreamWaitEvent(P->side, e, 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream fork failed");
+        for (int i = 1; i < ch.n; ++i) ERGM_TRY(fork_side(P, ch.s[i]));
+        P->stage_pt = e;  // the end of the stage on ch.s[0]: nothing more is enqueued there in this call
+    }
+    const int n = P->ln_pending;
     P->ln_pending = 0;
-    P->bias_pending = 0;
-    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side, nb,
-                                    P->bp_part, P->bp_rows, P->bp_cols, P->bp_out);
+    return layernorm_param_reduce_n(n, P->lnr_pg, P->lnr_pb, P->T, P->d.n_embd, P->lnr_dg, P->lnr_db, P->side);
 }
 
 
@@ -822,11 +785,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->need = 0;
     P->have_fwd = false;
     P->ln_pending = 0;
-    // weight-gradient biases as per-tile-row partials (no [K+1]-th tile row): ERGM_BIAS_ROWS=0 restores the ones row
-    P->bias_rows = true;
-    if (const char* e = getenv("ERGM_BIAS_ROWS")) P->bias_rows = atoi(e) != 0;
-    P->bias_k = 0;
-    P->bias_pending = 0;
     // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py lays the
     // flat buffers out that way) and a ones column in the activations (set here; producers write columns
     // < E / < F only); other layouts take the in-GEMM column sums (ergm_gemm_desc.bias_grad).
@@ -1303,7 +1261,8 @@ extern "C" int ergm_model_forward(ergm_model_plan* P, void* logits, float* emo_l
     ERGM_CHECK_ARG(P && logits && emo_logits, "model_forward: null argument");
     ERGM_CHECK_ARG(P->ids, "model_forward: call ergm_model_set_inputs first");
     ERGM_CHECK_ARG(!(P->labels || P->emo_labels) || out_loss, "model_forward: labels need out_loss");
-    bind_clear();  // a fork point is armed and taken inside one native call
+    bind_clear();
+    P->stage_pt = nullptr;  // a fork point is armed and taken inside one native call
     return do_forward(P, logits, emo_logits, out_loss, train, as_stream(stream));
 }
 
@@ -1312,8 +1271,6 @@ namespace {
 int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
     const ergm_model_dims& d = P->d;
     P->ln_pending = 0;
-    P->bias_pending = 0;
-    P->bias_k = 0;
     P->bwd_forked = false;
     const ergm_model_params& p = P->p;
     const int T = P->T, E = d.n_embd, B = d.batch, S = d.seq, Vp = d.vocab_pad, L = d.n_layer;
@@ -1523,7 +1480,6 @@ int do_backward_embed(ergm_model_plan* P, hipStream_t s) {
         const Chains one{1, {s, s}, {0, 0}, {d.batch, 0}};
         ERGM_TRY(dw_gemm(P, one, E, L2E, P->cap, P->XE, P->dkv_all, L2E, p.g_capkv_w, p.g_capkv_b));
         ERGM_TRY(dw_flush(P, one));
-        ERGM_TRY(ln_reduce_flush(P, one));  // its bias partials (no LayerNorm is pending here)
         ERGM_TRY(gemm(P, s, T, E, L2E, P->dkv_all, L2E, ERGM_MK, p.capkv_w_b, L2E, ERGM_NK, P->dcap, E, ERGM_F32,
                       ERGM_EPI_NONE));
     }
@@ -1575,18 +1531,18 @@ extern "C" int ergm_model_set_optimizer(ergm_model_plan* P, const ergm_adamw_des
 }
 
 namespace {
-// The optimizer stream waits for a bucket's gradients and for the last reader of its parameters.  mark >= 0: the
-// side stream's mark of that stage (a block l, L+1 = the LM-head dW) — recorded behind the stage's final fork from
-// the data-gradient chain(s) (the LayerNorm reduce after ln_1's backward; the LM-head dW after the LM-head dX),
-// so it also covers every data-gradient launch of the stage, on every chain.  mark < 0: everything issued so far
-// on `s` (a fresh event).
+// The optimizer stream waits for everything issued so far on `s` — the stage just enqueued, so a bucket's update
+// launched `lag` stages after its block overlaps the later blocks (opt_after_layer) — and, for mark >= 0, for the side
+// stream's weight-gradient mark of that stage (its gradients).  The point on `s` is the stage's final fork point
+// taken in this same native call (ln_reduce_flush: nothing has been enqueued on s since), else a fresh event.
 int opt_wait(ergm_model_plan* P, hipStream_t s, int mark) {
-    if (mark >= 0)
-        return hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) == hipSuccess
-                   ? ERGM_OK
-                   : fail(ERGM_EHIP, "model: optimizer stream wait");
-    hipEvent_t e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
-    if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess)
+    hipEvent_t e = P->stage_pt;
+    if (!e) {
+        e = P->ev_opt[P->opt_k++ % P->ev_opt.size()];
+        if (hipEventRecord(e, s) != hipSuccess) return fail(ERGM_EHIP, "model: optimizer stream wait");
+    }
+    if (hipStreamWaitEvent(P->opt_s, e, 0) != hipSuccess) return fail(ERGM_EHIP, "model: optimizer stream wait");
+    if (mark >= 0 && hipStreamWaitEvent(P->opt_s, P->ev_join[mark], 0) != hipSuccess)
         return fail(ERGM_EHIP, "model: optimizer stream wait");
     return ERGM_OK;
 }
@@ -1672,6 +1628,7 @@ extern "C" int ergm_model_backward_head(ergm_model_plan* P, const float* gscale,
     ERGM_CHECK_ARG(P, "model_backward_head: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_head: no training forward to differentiate");
     bind_clear();
+    P->stage_pt = nullptr;
     return do_backward_head(P, gscale, as_stream(stream));
 }
 
@@ -1679,6 +1636,7 @@ extern "C" int ergm_model_backward_layer(ergm_model_plan* P, int layer, void* st
     ERGM_CHECK_ARG(P && layer >= 0 && layer < P->d.n_layer, "model_backward_layer: bad layer");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_layer: no training forward to differentiate");
     bind_clear();
+    P->stage_pt = nullptr;
     ERGM_TRY(do_backward_layer(P, layer, as_stream(stream)));
     return opt_after_layer(P, layer, as_stream(stream));
 }
@@ -1687,6 +1645,7 @@ extern "C" int ergm_model_backward_embed(ergm_model_plan* P, void* stream) {
     ERGM_CHECK_ARG(P, "model_backward_embed: null plan");
     ERGM_CHECK_ARG(P->have_fwd, "model_backward_embed: no training forward to differentiate");
     bind_clear();
+    P->stage_pt = nullptr;
     ERGM_TRY(do_backward_embed(P, as_stream(stream)));
     return opt_after_embed(P, as_stream(stream));
 }

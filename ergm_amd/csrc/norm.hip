@@ -241,44 +241,34 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
     }
 }
 
-// Column reductions out[c] = Σ_r part[r][c] (rows in fixed order, deterministic), up to 16 jobs per launch: the
-// LayerNorms' dγ / dβ from their per-8-row partials and the weight-gradient bias partials of a backward stage
-// (ergm_gemm_desc.bias_part), in ONE launch per stage.  Workgroup b works on 32 columns of the job whose block range
-// holds b.
-struct ColReduceJob {
-    const float* part;  // [rows][cols]
-    float* out;         // [cols]
-    int rows, cols;
-    int blk0;           // first workgroup of this job
-};
-struct ColReduceJobs {
-    ColReduceJob j[16];
-    int n;
+// dγ / dβ: sum the per-block partials (fixed order).  grid (cdiv(E,64), 2), 1024 threads: 64 columns x
+// 16 row lanes, each lane with 16 partial rows in flight per round (one HBM latency per 256 partials).
+struct LnReduceJobs {  // up to 4 LayerNorms' (partials, dγ, dβ) reduced by one launch (blockIdx.z)
+    const float* part_g[4];
+    const float* part_b[4];
+    float* dgamma[4];
+    float* dbeta[4];
 };
 
 // 256-thread blocks (32 columns x 8 row lanes): small enough to find free wave slots beside the GEMMs running
 // concurrently on the other streams (a 1024-thread block needs a whole CU's slots and waited behind long GEMM tiles
 // at config-5 sizes).  Each lane keeps LN_RED_LOADS partial rows in flight per round, so the training step's 256
-// LayerNorm partial rows (T = 2048) are one round: one memory latency per launch instead of two (round 4: 16 per
-// lane, two dependent rounds, 19.5 us in-step).
+// partial rows (T = 2048) are one round: one memory latency per launch instead of two (round 4: 16 per lane).
 constexpr int LN_RED_LOADS = 32;
-__global__ __launch_bounds__(256) void col_reduce_kernel(ColReduceJobs jobs) {
+__global__ __launch_bounds__(256) void ln_param_reduce_kernel(LnReduceJobs jobs, int nparts, int E) {
     __shared__ float red[8][32];
-    int ji = 0;
-#pragma unroll 1
-    for (int i = 1; i < jobs.n; ++i)
-        if ((int)blockIdx.x >= jobs.j[i].blk0) ji = i;
-    const ColReduceJob& J = jobs.j[ji];
+    const int z = blockIdx.z;
+    const float* part = blockIdx.y == 0 ? jobs.part_g[z] : jobs.part_b[z];
+    float* out = blockIdx.y == 0 ? jobs.dgamma[z] : jobs.dbeta[z];
     const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
-    const int c = ((int)blockIdx.x - J.blk0) * 32 + cl;
-    const float* part = J.part;
+    const int c = blockIdx.x * 32 + cl;
     float acc = 0.f;
-    for (int base = 0; base < J.rows; base += 8 * LN_RED_LOADS) {
+    for (int base = 0; base < nparts; base += 8 * LN_RED_LOADS) {
         float v[LN_RED_LOADS];
 #pragma unroll
         for (int j = 0; j < LN_RED_LOADS; ++j) {
             const int r = base + rl + 8 * j;
-            v[j] = c < J.cols && r < J.rows ? __builtin_nontemporal_load(part + (size_t)r * J.cols + c) : 0.f;
+            v[j] = c < E && r < nparts ? __builtin_nontemporal_load(part + (size_t)r * E + c) : 0.f;
         }
 #pragma unroll
         for (int w = 1; w < LN_RED_LOADS; w <<= 1)
@@ -288,7 +278,7 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(ColReduceJobs jobs) {
     }
     red[rl][cl] = acc;
     __syncthreads();
-    if (rl == 0 && c < J.cols) {
+    if (rl == 0 && c < E) {
         float t[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) t[j] = red[j][cl];
@@ -296,7 +286,7 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(ColReduceJobs jobs) {
         for (int w = 1; w < 8; w <<= 1)
 #pragma unroll
             for (int j = 0; j < 8; j += 2 * w) t[j] += t[j + w];
-        J.out[c] = t[0];
+        out[c] = t[0];
     }
 }
 
@@ -464,34 +454,20 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
 }
 
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
-                             float* const* dgamma, float* const* dbeta, hipStream_t s, int nb, const float* const* bpart,
-                             const int* brows, const int* bcols, float* const* bout) {
-    ERGM_CHECK_ARG(n >= 0 && n <= 4 && nb >= 0 && nb <= 8 && n + nb > 0,
-                   "layernorm_param_reduce: 0..4 LayerNorms and 0..8 bias jobs per launch");
-    ColReduceJobs j{};
-    int blk = 0;
-    auto add = [&](const float* part, float* out, int r, int cols) {
-        ColReduceJob& J = j.j[j.n++];
-        J.part = part; J.out = out; J.rows = r; J.cols = cols; J.blk0 = blk;
-        blk += cdiv(cols, 32);
-    };
+                             float* const* dgamma, float* const* dbeta, hipStream_t s) {
+    ERGM_CHECK_ARG(n >= 1 && n <= 4, "layernorm_param_reduce: 1..4 jobs per launch");
+    LnReduceJobs j{};
     for (int i = 0; i < n; ++i) {
         ERGM_CHECK_ARG(part_g[i] && part_b[i] && dgamma[i] && dbeta[i], "layernorm_param_reduce: null argument");
-        add(part_g[i], dgamma[i], ln_bwd_nparts(rows), E);
-        add(part_b[i], dbeta[i], ln_bwd_nparts(rows), E);
+        j.part_g[i] = part_g[i]; j.part_b[i] = part_b[i]; j.dgamma[i] = dgamma[i]; j.dbeta[i] = dbeta[i];
     }
-    for (int i = 0; i < nb; ++i) {
-        ERGM_CHECK_ARG(bpart[i] && bout[i] && brows[i] > 0 && bcols[i] > 0, "layernorm_param_reduce: bad bias job");
-        add(bpart[i], bout[i], brows[i], bcols[i]);
-    }
-    ERGM_LAUNCH(col_reduce_kernel, dim3(blk), dim3(256), 0, s, j);
+    ERGM_LAUNCH(ln_param_reduce_kernel, dim3(cdiv(E, 32), 2, n), dim3(256), 0, s, j, ln_bwd_nparts(rows), E);
     return check_launch("layernorm_param_reduce");
 }
 
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s) {
-    return layernorm_param_reduce_n(1, &part_g, &part_b, rows, E, &dgamma, &dbeta, s, 0, nullptr, nullptr, nullptr,
-                                    nullptr);
+    return layernorm_param_reduce_n(1, &part_g, &part_b, rows, E, &dgamma, &dbeta, s);
 }
 }  // namespace ergm
 

@@ -33,11 +33,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int
          out: Optional[torch.Tensor] = None, out_dtype=torch.float32, epilogue: int = L.EPI_NONE,
          bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
          aux_out: Optional[torch.Tensor] = None, alpha: float = 1.0, split_k: int = 0,
-         alpha_dev: Optional[torch.Tensor] = None, bias_grad: Optional[torch.Tensor] = None,
-         bias_part: Optional[torch.Tensor] = None) -> torch.Tensor:
+         alpha_dev: Optional[torch.Tensor] = None, bias_grad: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C[M,N] = epilogue(alpha · A·B); A/B bf16 row-major with layouts as in ergm_hip.h.  ``bias_grad`` (f32 [N],
-    KM x KN weight gradients only) also receives alpha·Σ_k B[k][n]; ``bias_part`` (f32 [gemm_bias_rows(..)][N])
-    receives it as per-tile-row partial sums over disjoint token ranges."""
+    KM x KN weight gradients only) also receives alpha·Σ_k B[k][n]."""
     _need_gpu(A, B)
     assert A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
     lda = A.stride(0) if A.dim() == 2 else (K if a_layout == L.MK else M)
@@ -48,19 +46,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, M: int, N: int, K: int, a_layout: int
                    c_dtype=L.BF16 if out.dtype == torch.bfloat16 else L.F32, epilogue=epilogue, alpha=alpha,
                    bias=_ptr(bias), aux=_ptr(aux), ld_aux=aux.stride(0) if aux is not None else 0,
                    aux_out=_ptr(aux_out), ld_aux_out=aux_out.stride(0) if aux_out is not None else 0,
-                   split_k=split_k, alpha_dev=_ptr(alpha_dev), bias_grad=_ptr(bias_grad), bias_part=_ptr(bias_part))
+                   split_k=split_k, alpha_dev=_ptr(alpha_dev), bias_grad=_ptr(bias_grad))
     lib = L.load()
     wsb = lib.ergm_gemm_workspace_size(C.byref(d))
     ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=A.device)
     L.check(lib.ergm_gemm(C.byref(d), _ptr(A), _ptr(B), _ptr(out), _ptr(ws), wsb, _stream(A.device)), "ergm_gemm")
     return out
-
-
-def gemm_bias_rows(M: int, N: int, K: int, lda: int = 0, ldb: int = 0) -> int:
-    """ergm_gemm_bias_rows of a KM x KN weight-gradient GEMM (f32 out): the rows of its bias_part, 0 if none."""
-    d = L.GemmDesc(M=M, N=N, K=K, lda=lda or (M + 7) // 8 * 8, ldb=ldb or N, ldc=N, a_layout=L.KM, b_layout=L.KN,
-                   c_dtype=L.F32, epilogue=L.EPI_NONE, alpha=1.0)
-    return int(L.load().ergm_gemm_bias_rows(C.byref(d)))
 
 
 def gemm_f8(A8: torch.Tensor, a_scale: torch.Tensor, B8t: torch.Tensor, b_scale: torch.Tensor,

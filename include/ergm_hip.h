@@ -124,17 +124,7 @@ typedef struct {
                           * also write alpha·Σ_k B[k][n] (the Conv1D bias gradient, column sums of dY over
                           * the K tokens) to bias_grad[n], f32 [N]; NULL = none.  Computed from the B
                           * fragments the GEMM already stages (no second pass over dY), deterministic. */
-    float* bias_part;    /* the same layouts, bias_grad NULL: the bias gradient as per-tile-row partial column
-                          * sums, bias_part[r][n] for r < ergm_gemm_bias_rows(desc), row r summing a disjoint
-                          * range of the K tokens (alpha applied) — every tile row shares the work, so a
-                          * [K_in][N] weight gradient needs no extra [K_in+1]-th tile row for its bias; the caller
-                          * adds the rows in order (deterministic).  NULL = none (ABI 9). */
 } ergm_gemm_desc;
-
-/* Rows of ergm_gemm_desc.bias_part the planned GEMM writes for `desc` (its bias_part field ignored): the tile-row
- * count of the pipelined kernel it plans to, or 0 when that plan cannot write them (register-staged or split-K
- * plans: pass bias_grad, or an augmented ones row, instead).                                            */
-int ergm_gemm_bias_rows(const ergm_gemm_desc* desc);
 
 /* Tuning hook (calling thread only): force pipelined-kernel configuration `cfg` (tile / wave grid /
  * LDS stages, see kCfgs in ergm_amd/csrc/gemm.hip) and split-K count for later ergm_gemm calls;

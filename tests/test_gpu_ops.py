@@ -119,43 +119,6 @@ def test_gemm_bias_grad(gpu, M, N, K, split, cfg):
         ops.gemm(X.t().contiguous(), dY, M, N, K, a_layout=L.MK, b_layout=L.KN, bias_grad=db)
 
 
-@pytest.mark.parametrize("M,N,K,cfg", [(769, 3072, 2048, -1), (3073, 768, 2048, -1), (769, 768, 2048, -1),
-                                       (769, 2304, 2048, -1), (769, 768, 4096, -1), (200, 136, 1024, 0),
-                                       (257, 512, 1024, 10), (257, 512, 128, 2), (769, 768, 1000, -1)])
-def test_gemm_bias_part_rows(gpu, M, N, K, cfg):
-    """ergm_gemm_desc.bias_part: the weight gradient's bias as per-tile-row partial column sums — every tile row sums
-    its own share of the K tokens (the executor's default, no augmented [K+1]-th tile row).  The rows (all written)
-    sum in row order to Σ_t dY[t] within fp32 rounding of fp64, dW is bitwise the plain GEMM's (the summing waves run
-    the same MFMA order), reproducible; a plan without the per-row sums (K % 64 != 0: register-staged) reports 0 rows
-    and rejects bias_part."""
-    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
-    ld = (M + 7) // 8 * 8
-    X = (torch.randn(K, ld, generator=g) * 0.5).to(gpu, torch.bfloat16)[:, :M]
-    dY = (torch.randn(K, N, generator=g) * 0.5).to(gpu, torch.bfloat16)
-    L.check(L.load().ergm_gemm_tune(cfg, 0), "tune")
-    try:
-        rows = ops.gemm_bias_rows(M, N, K, lda=ld)
-        if K % 64:
-            assert rows == 0
-            with pytest.raises(ValueError):
-                ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, bias_part=torch.zeros(1, N, device=gpu))
-            return
-        assert rows >= 1
-        part = torch.full((rows, N), float("nan"), device=gpu)
-        dW = ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, bias_part=part)
-        part2 = torch.full((rows, N), float("nan"), device=gpu)
-        dW2 = ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN, bias_part=part2)
-        plain = ops.gemm(X, dY, M, N, K, a_layout=L.KM, b_layout=L.KN)
-    finally:
-        L.load().ergm_gemm_tune(-1, 0)
-    torch.cuda.synchronize()
-    assert not torch.isnan(part).any()
-    assert torch.equal(dW, plain) and torch.equal(dW2, plain) and torch.equal(part, part2)
-    ref_b = dY.double().sum(0)
-    got = part.double().sum(0)
-    assert ((got - ref_b).abs() / (ref_b.abs() + 1.0)).max().item() < 1e-4
-
-
 def test_gemm_epilogues(gpu):
     M, N, K = 256, 384, 192
     A = torch.randn(M, K, device=gpu).bfloat16()
