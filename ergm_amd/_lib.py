@@ -109,6 +109,8 @@ _SIGS = {
     "ergm_chunk_sum_bf16": (i32, [vp, i32, sz, vp, vp]),
     "ergm_chunk_sum_bf16_f32": (i32, [vp, i32, sz, sz, vp, vp]),
     "ergm_cast_f32": (i32, [vp, vp, sz, vp]),
+    "ergm_dp_pack_bf16": (i32, [vp, sz, vp, sz, vp]),
+    "ergm_dp_sum_adamw": (i32, [vp, i32, sz, sz, vp, vp, vp, vp, vp, f64, f64, f64, f32, f64, f32, f32, vp]),
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),

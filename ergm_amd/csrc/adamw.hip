@@ -228,6 +228,46 @@ __global__ __launch_bounds__(256) void chunk_sum_f32_kernel(const bf16x4* __rest
     }
 }
 
+// ZeRO-1 bucket, one launch instead of the chunk sum + the shard's AdamW pass: the reduced gradient of this rank's
+// chunk (the chunk_sum_f32_kernel value, bitwise) is written into the fp32 gradient and applied to the shard's
+// parameters / moments in the same pass, the updated bf16 parameters going straight into this rank's all-gather slot.
+__global__ __launch_bounds__(256) void dp_sum_adamw_kernel(const bf16x4* __restrict__ in, int nchunks, size_t chunk4,
+                                                           size_t n4, float4* __restrict__ grad, float4* __restrict__ p,
+                                                           float4* __restrict__ m, float4* __restrict__ v,
+                                                           bf16x4* __restrict__ shadow, AdamScalars sc) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < nchunks; ++j) {
+            const bf16x4 w = in[(size_t)j * chunk4 + i];
+            s.x += bf2f(w[0]); s.y += bf2f(w[1]); s.z += bf2f(w[2]); s.w += bf2f(w[3]);
+        }
+        const float4 g = make_float4(bf2f(f2bf(s.x)), bf2f(f2bf(s.y)), bf2f(f2bf(s.z)), bf2f(f2bf(s.w)));
+        grad[i] = g;
+        float4 pp = nt_load4(p + i), mm = nt_load4(m + i), vv = nt_load4(v + i);
+        bf16x4 o;
+        adamw_one(pp, g, mm, vv, o, sc);
+        nt_store4(p + i, pp);
+        nt_store4(m + i, mm);
+        nt_store4(v + i, vv);
+        shadow[i] = o;
+    }
+}
+
+// Pack a bucket for the all-to-all: dst[i] = bf16(src[i]) for i < n, 0 up to `total` (the padded W x chunk).
+__global__ __launch_bounds__(256) void dp_pack_kernel(const float4* __restrict__ src, size_t n4, bf16x4* __restrict__ dst,
+                                                      size_t total4) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total4; i += (size_t)gridDim.x * 256) {
+        bf16x4 o;
+        if (i < n4) {
+            const float4 x = src[i];
+            o[0] = f2bf(x.x); o[1] = f2bf(x.y); o[2] = f2bf(x.z); o[3] = f2bf(x.w);
+        } else {
+            o[0] = o[1] = o[2] = o[3] = f2bf(0.f);
+        }
+        dst[i] = o;
+    }
+}
+
 __global__ __launch_bounds__(256) void cast_f32_kernel(const bf16x4* __restrict__ src, float4* __restrict__ dst,
                                                        size_t n4) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
@@ -263,4 +303,30 @@ extern "C" int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream
     ERGM_LAUNCH(cast_f32_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)src,
                        (float4*)dst, n4);
     return check_launch("cast_f32");
+}
+
+extern "C" int ergm_dp_pack_bf16(const float* src, size_t n, void* dst, size_t total, void* stream) {
+    ERGM_CHECK_ARG(src && dst && n % 4 == 0 && total % 4 == 0 && n <= total, "dp_pack_bf16: bad argument");
+    ERGM_CHECK_ARG(aligned16(src) && (reinterpret_cast<uintptr_t>(dst) & 7) == 0, "dp_pack_bf16: alignment");
+    const size_t t4 = total / 4;
+    if (t4 == 0) return ERGM_OK;
+    ERGM_LAUNCH(dp_pack_kernel, dim3(grid_for(t4)), dim3(256), 0, as_stream(stream), (const float4*)src, n / 4,
+                (bf16x4*)dst, t4);
+    return check_launch("dp_pack_bf16");
+}
+
+extern "C" int ergm_dp_sum_adamw(const void* in, int nchunks, size_t chunk, size_t n, float* grad, float* p, float* m,
+                                 float* v, void* shadow, double lr, double beta1, double beta2, float eps,
+                                 double weight_decay, float step_size, float bc2_sqrt, void* stream) {
+    ERGM_CHECK_ARG(in && grad && p && m && v && shadow && nchunks > 0 && chunk % 4 == 0 && n % 4 == 0 && n <= chunk,
+                   "dp_sum_adamw: bad argument");
+    ERGM_CHECK_ARG(aligned16(grad) && aligned16(p) && aligned16(m) && aligned16(v) &&
+                       (reinterpret_cast<uintptr_t>(shadow) & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 7) == 0,
+                   "dp_sum_adamw: alignment");
+    const size_t n4 = n / 4;
+    if (n4 == 0) return ERGM_OK;
+    const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
+    ERGM_LAUNCH(dp_sum_adamw_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in, nchunks,
+                chunk / 4, n4, (float4*)grad, (float4*)p, (float4*)m, (float4*)v, (bf16x4*)shadow, sc);
+    return check_launch("dp_sum_adamw");
 }

@@ -1067,7 +1067,11 @@ static constexpr GemmOverride kStepTuned[] = {
     {769, 768, 2048, ERGM_KM, ERGM_KN, 11, 1},   // attn c_proj / q / cross c_proj weight gradients (round 4)
     {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
     {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1},
-    {4096, 1024, 4096, ERGM_MK, ERGM_NK, 2, 1},  // GPT-2-medium c_fc data gradient (C5, step_tune pass 2)
+    // config 5 (GPT-2-medium, B=32, T=4096) data gradients, round 5's re-tune on the current build (tools/step_tune.py
+    // --config c5: 21.53 -> 21.11 ms/step in the tuner, profiles/r05_step_tune_c5.txt)
+    {4096, 1024, 4096, ERGM_MK, ERGM_NK, 15, 1}, // c_fc data gradient (cfg 2 since round 1's pass 2)
+    {4096, 4096, 1024, ERGM_MK, ERGM_NK, 6, 1},  // mlp c_proj data gradient (GELU' epilogue)
+    {4096, 1024, 3072, ERGM_MK, ERGM_NK, 2, 1},  // c_attn data gradient
     {50304, 768, 4096, ERGM_KM, ERGM_KN, 4, 1},  // LM-head weight gradient at T = 4096 (C4)
     // config 4 (S = 512, T = 4096), round 4's re-tune (profiles/r04_step_tune_c4.txt, experiments #26)
     {4096, 3072, 768, ERGM_MK, ERGM_NK, 2, 1},   // mlp c_proj data gradient (GELU' epilogue)

@@ -281,6 +281,9 @@ class DPSync:
         reduce-scatter, update of this rank's chunk, all-gather of the updated bf16 ``shadow`` chunks)
         when enabled, otherwise on the whole all-reduced range."""
         if self.active and self.zero and post is not None and shadow is not None:
+            if grad.is_cuda and getattr(post, "native", None) is not None:
+                self._zero_bucket_native(grad, a, b, post.native, shadow)
+                return
             lo, hi = self.reduce_scatter_(grad[a:b])
             if grad.is_cuda:  # the update writes its bf16 shadow chunk straight into its all-gather slot
                 n = b - a
@@ -305,6 +308,36 @@ class DPSync:
             post(a, b)
         self.sharded.discard((a, b))
         self.master_sharded.discard((a, b))
+
+    def _zero_bucket_native(self, grad: torch.Tensor, a: int, b: int, nat: dict, shadow: torch.Tensor) -> None:
+        """ZeRO-1 bucket [a, b) with the host work cut to two native calls around the two collectives: pack (cast +
+        zero padding) -> all-to-all -> rank-order sum + this rank's AdamW shard + its bf16 all-gather slot
+        (ergm_dp_sum_adamw, bitwise the chunk sum then ergm_adamw_step) -> all-gather -> shadow copy.  The numbers
+        are those of reduce_scatter_ + post + _gather."""
+        import torch.distributed as dist
+        from . import _lib as L
+        W, n = self.world, b - a
+        chunk = self.chunk(n)
+        lo, hi = self.shard(n)
+        send, recv, gath = self._buffers(chunk, grad.device)
+        mine = gath.view(W, chunk)[self.rank]
+        st = C.c_void_p(torch.cuda.current_stream(grad.device).cuda_stream)
+        g0 = grad.data_ptr()
+        L.call("ergm_dp_pack_bf16", C.c_void_p(g0 + 4 * a), n, C.c_void_p(send.data_ptr()), W * chunk, st)
+        dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+        if hi > lo:
+            o = 4 * (a + lo)
+            L.call("ergm_dp_sum_adamw", C.c_void_p(recv.data_ptr()), W, chunk, hi - lo, C.c_void_p(g0 + o),
+                   C.c_void_p(nat["p"].data_ptr() + o), C.c_void_p(nat["m"].data_ptr() + o),
+                   C.c_void_p(nat["v"].data_ptr() + o), C.c_void_p(mine.data_ptr()), nat["lr"], nat["beta1"],
+                   nat["beta2"], nat["eps"], nat["weight_decay"], nat["step_size"], nat["bc2_sqrt"], st)
+        self.bytes_per_step += 2 * (W - 1) * chunk * 2
+        dist.all_gather_into_tensor(gath, mine, group=self.pg, async_op=True).wait()
+        shadow[a:b].copy_(gath[:n])
+        if self._master is not None:
+            self._pend_master.append((a, b, lo, hi))
+        self.sharded.add((a, b))
+        self.master_sharded.add((a, b))
 
     def consolidate_(self, tensors, ranges=None) -> None:
         """All-gather the owners' chunks of every sharded range into each fp32 tensor (master, gradient,

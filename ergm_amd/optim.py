@@ -158,6 +158,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 row_len, flags, select = rows
                 ops.adamw_rows(flat.data[a:b], g[a:b], m[a:b], v[a:b], shadow[a:b], row_len, flags, select, lr, b1,
                                b2, eps, wd, t, nb)
+        # what a fused native exchange (dist.DPSync, ergm_dp_sum_adamw) needs to apply the same update itself
+        post.native = dict(p=flat.data, m=m, v=v, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
+                           step_size=lr / (1 - b1 ** t), bc2_sqrt=math.sqrt(1 - b2 ** t))
         return post
 
     def _native_desc(self, flat, model):
