@@ -335,9 +335,23 @@ def main():
     torch.cuda.synchronize()
     sync0 = sum(r.host_sync_s for r in model._runners.values())
     prof = None
+    prof_bwd = None
     if os.environ.get("ERGM_BENCH_CPROFILE"):  # host-cost diagnostics: cProfile of the timed loop only
         import cProfile
+        from ergm_amd import runtime as _rt
         prof = cProfile.Profile()
+        # the backward (native stages + the data-parallel exchange) runs on autograd's device thread, which the
+        # main thread's profiler does not see: a second profiler inside ModelRunner.backward
+        prof_bwd = cProfile.Profile()
+        _bwd = _rt.ModelRunner.backward
+
+        def _prof_backward(self, *a, **k):
+            prof_bwd.enable()
+            try:
+                return _bwd(self, *a, **k)
+            finally:
+                prof_bwd.disable()
+        _rt.ModelRunner.backward = _prof_backward
         prof.enable()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -349,6 +363,8 @@ def main():
     if prof is not None:
         prof.disable()
         prof.dump_stats(os.environ["ERGM_BENCH_CPROFILE"])
+        prof_bwd.dump_stats(os.environ["ERGM_BENCH_CPROFILE"] + ".bwd")
+        _rt.ModelRunner.backward = _bwd
     t_sync = sum(r.host_sync_s for r in model._runners.values()) - sync0  # of it: waiting (DP row count)
     torch.cuda.synchronize()
     barrier()

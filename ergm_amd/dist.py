@@ -69,6 +69,8 @@ class DPSync:
         # host ~0.15 ms of Python / ctypes / collective calls, which at 14 buckets per step left the host at
         # ~90 % of the GPU step under DP (bench ERGM_BENCH_FAKE_PG); two blocks per exchange halve that
         self.merge = max(1, int(os.environ.get("ERGM_DP_MERGE", "2")))
+        # ZeRO-1 buckets through the fused native calls (_zero_bucket_native); ERGM_DP_NATIVE=0: the Python sequence
+        self.native = os.environ.get("ERGM_DP_NATIVE", "1") != "0"
         self._pend_a: Optional[int] = None
         # flat ranges [a, b) whose last update ran shard-wise: gradient and optimizer moments stale outside
         # this rank's chunk (sharded), and the fp32 master too until a load_state_dict rewrites it
@@ -281,7 +283,7 @@ class DPSync:
         reduce-scatter, update of this rank's chunk, all-gather of the updated bf16 ``shadow`` chunks)
         when enabled, otherwise on the whole all-reduced range."""
         if self.active and self.zero and post is not None and shadow is not None:
-            if grad.is_cuda and getattr(post, "native", None) is not None:
+            if grad.is_cuda and self.native and getattr(post, "native", None) is not None:
                 self._zero_bucket_native(grad, a, b, post.native, shadow)
                 return
             lo, hi = self.reduce_scatter_(grad[a:b])

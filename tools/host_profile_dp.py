@@ -14,5 +14,8 @@ if n != "1":
 subprocess.run([sys.executable, os.path.join(here, "bench.py"), "--no-cpu-baseline", "--steps", "20", "--warmup", "3",
                 "--no-gpu-only"], env=env, check=True, stdout=subprocess.DEVNULL)
 p = pstats.Stats("/tmp/dp.prof")
-p.sort_stats("tottime").print_stats(40)
-p.sort_stats("cumulative").print_stats(30)
+p.sort_stats("tottime").print_stats(25)
+print("==== backward (autograd's thread: native stages + data-parallel exchange) ====")
+q = pstats.Stats("/tmp/dp.prof.bwd")
+q.sort_stats("tottime").print_stats(45)
+q.sort_stats("cumulative").print_stats(30)
