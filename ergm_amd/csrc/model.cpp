@@ -47,9 +47,10 @@ int quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void
                    hipStream_t s);
 int fill_ones_col(void* p, int rows, int ld, int col, hipStream_t s);
 int ln_bwd_nparts(int rows);
-int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
-                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs);
+int ln_bwd_rows_per_part();
+int layernorm_bwd_main(const void* dy, int dy_bf16, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E,
+                       hipStream_t s, const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs);
 int layernorm_param_reduce(const float* part_g, const float* part_b, int rows, int E, float* dgamma, float* dbeta,
                            hipStream_t s);
 int layernorm_param_reduce_n(int n, const float* const* part_g, const float* const* part_b, int rows, int E,
@@ -170,6 +171,7 @@ struct ergm_model_plan {
     float* lookup_compact;
     // backward scratch
     float *dh, *dy, *dcap, *delta;
+    __bf16* dyb;  // the block LayerNorms' incoming gradient: their data-gradient GEMM's bf16 output (ln_f's: dy, f32)
     __bf16 *d_o, *dkv_all;
     // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
     // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
@@ -329,7 +331,7 @@ size_t carve(ergm_model_plan* P, char* base) {
     P->keys = c.take<uint64_t>(embed_sort_capacity(T));
     P->mwords = (d.seq + 63) / 64;
     P->abits = c.take<uint64_t>((size_t)2 * L * BHS * P->mwords);
-    P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dcap = c.take<float>(T * E);
+    P->dh = c.take<float>(T * E); P->dy = c.take<float>(T * E); P->dyb = c.take<__bf16>(T * E); P->dcap = c.take<float>(T * E);
     P->delta = c.take<float>(BHS);
     P->d_o = c.take<__bf16>(T * E);
     P->dkv_all = c.take<__bf16>(T * 2 * E * L);
@@ -600,13 +602,16 @@ int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* 
     const int T = P->T, E = P->d.n_embd;
     float* pg = P->ln_part[slot];
     float* pb = pg + (size_t)ln_bwd_nparts(T) * E;
-    const size_t o = (size_t)r0 * E, po = (size_t)(r0 / 8) * E;
+    const size_t o = (size_t)r0 * E, po = (size_t)(r0 / ln_bwd_rows_per_part()) * E;
     // dh_b feeds the residual branch that produced this residual-stream tensor (slot = its index):
     // through that branch's dropout.  Slot 0 (the embeddings) has no bf16 consumer: there the final dh
     // itself goes through the embedding dropout (src/model.py:506), folded into this pass.
     const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
     const int fin = slot == 0;
-    return layernorm_bwd_main(P->dy + o, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
+    // the block LayerNorms read their data-gradient GEMM's bf16 output (as the reference's autocast GEMM backward
+    // hands LayerNorm a bf16 gradient); ln_f (slot 3L) the f32 sum of the LM-head and emotion-head gradients
+    const bool yb = slot != 3 * P->d.n_layer;
+    return layernorm_bwd_main(yb ? (const void*)(P->dyb + o) : (const void*)(P->dy + o), yb, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
                               pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin, nullptr, nullptr, T);
 }
 int ln_reduce_add(ergm_model_plan* P, int slot, float* dgamma, float* dbeta) {
@@ -1339,6 +1344,8 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // per-chain row offset helper (dry run: pointers stay null)
     auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
     auto Tc = [&](int c) { return ch.nb[c] * S; };
+    // the block LayerNorms' incoming gradient (ln_bwd_rows reads the same buffer)
+    auto DYO = [&](int c) { return R(P->dyb, c, E); };
     // Weight-gradient pairs (mlp c_proj + c_fc, cross c_proj + q, attn c_proj + c_attn) are forked to the side
     // stream once the dY of the second member is formed.
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
@@ -1354,7 +1361,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
-                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+                      DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
@@ -1392,7 +1399,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
-                      R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+                      DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
@@ -1430,7 +1437,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
-                      ERGM_NK, R(P->dy, c, E), E, ERGM_F32, ERGM_EPI_NONE));
+                      ERGM_NK, DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c) {
         if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));

@@ -9,7 +9,6 @@
 
 namespace ergm {
 
-constexpr int LN_ROWS_PER_BLOCK_BWD = 8;
 constexpr int LN_WAVES_BWD = 8;  // one row per wave: 8 waves per CU in flight at T = 2048
 
 template <int NV>
@@ -110,8 +109,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // dres_b = bf16(dres), or with `drop` the gradient reaching the residual branch that produced this
 // residual-stream tensor through its dropout: bf16(dres·keep/(1-p)) (src/model.py:245,266,506; the
 // keep bits recomputed, common.h drop_keep4).
-template <int NV>
-__global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+// DYB: dy is the bf16 output of the data-gradient GEMM (the per-block LayerNorms), else f32 (ln_f: the LM-head
+// and emotion-head gradients summed in f32).
+template <int NV, bool DYB, int RPW>
+__global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
                                                      __bf16* __restrict__ dres_b, float* __restrict__ part_g,
@@ -131,8 +132,7 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
     const float inv_e = 1.0f / (float)E;
     // each wave owns RPW rows and issues every load of all of them (x, dy and the residual gradient it
     // adds into) before the first reduction, so the HBM latency is paid once
-    constexpr int RPW = LN_ROWS_PER_BLOCK_BWD / LN_WAVES_BWD;
-    const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD + wave * RPW;
+    const int r0 = (blockIdx.x * LN_WAVES_BWD + wave) * RPW;
     float4 xh[RPW][NV], d[RPW][NV], o[RPW][NV];
     float mu[RPW], rs[RPW];
 #pragma unroll
@@ -146,7 +146,13 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const float* 
             int c = (i * 64 + lane) * 4;
             if (live && c < E) {
                 xh[j][i] = *reinterpret_cast<const float4*>(x + (size_t)row * E + c);
-                d[j][i] = *reinterpret_cast<const float4*>(dy + (size_t)row * E + c);
+                if constexpr (DYB) {
+                    const bf16x4 b = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(dy_) +
+                                                                      (size_t)row * E + c);
+                    d[j][i] = make_float4(bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3]));
+                } else {
+                    d[j][i] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy_) + (size_t)row * E + c);
+                }
                 o[j][i] = *reinterpret_cast<const float4*>(dres + (size_t)row * E + c);
             } else {
                 xh[j][i] = d[j][i] = o[j][i] = make_float4(0, 0, 0, 0);
@@ -423,8 +429,11 @@ extern "C" int ergm_layernorm_fwd(const float* x, const float* gamma, const floa
                             nullptr, 0);
 }
 
+namespace ergm {
+int ln_bwd_nparts(int rows);
+}
 extern "C" size_t ergm_layernorm_bwd_workspace_size(int rows, int E) {
-    int nb = cdiv(rows, LN_ROWS_PER_BLOCK_BWD);
+    int nb = ln_bwd_nparts(rows);
     return 2 * (size_t)nb * E * sizeof(float);
 }
 
@@ -432,11 +441,20 @@ namespace ergm {
 // Main LayerNorm-backward pass only: dres += dx, dres_bf16, and per-block dγ/dβ partials
 // (part_g/part_b: ln_bwd_nparts(rows) x E floats each), reduced later by layernorm_param_reduce.
 // drop_res: the updated dres is final and itself goes through `drop` (dres_bf16 then gets the same values).
-int ln_bwd_nparts(int rows) { return cdiv(rows, LN_ROWS_PER_BLOCK_BWD); }
+// Rows per workgroup: LN_WAVES_BWD waves of ln_bwd_rpw() rows each (ERGM_LN_RPW = 1 or 2).
+static int ln_bwd_rpw() {
+    static const int r = [] {
+        const char* e = getenv("ERGM_LN_RPW");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return r;
+}
+int ln_bwd_rows_per_part() { return LN_WAVES_BWD * ln_bwd_rpw(); }
+int ln_bwd_nparts(int rows) { return cdiv(rows, ln_bwd_rows_per_part()); }
 
-int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
-                       float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E, hipStream_t s,
-                       const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs) {
+int layernorm_bwd_main(const void* dy, int dy_bf16, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, float* dres, void* dres_bf16, float* part_g, float* part_b, int rows, int E,
+                       hipStream_t s, const DropSite& drop, int drop_res, void* qmx, void* qmx_s, int ld_qs) {
     ERGM_CHECK_ARG(dy && x && mean && rstd && gamma && dres && part_g && part_b, "layernorm_bwd: null argument");
     ERGM_CHECK_ARG(rows > 0 && E > 0 && E % 4 == 0 && E <= 1024, "layernorm_bwd: unsupported E=%d", E);
     ERGM_CHECK_ARG(!qmx || (dres_bf16 && qmx_s && E % 32 == 0 && ld_qs >= rows), "layernorm_bwd: bad MX-fp8 output");
@@ -444,12 +462,26 @@ int layernorm_bwd_main(const float* dy, const float* x, const float* mean, const
     auto* qs = reinterpret_cast<uint8_t*>(qmx_s);
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
-    switch (cdiv(E, 256)) {
-        case 1: ERGM_LAUNCH(ln_bwd_kernel<1>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
-        case 2: ERGM_LAUNCH(ln_bwd_kernel<2>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
-        case 3: ERGM_LAUNCH(ln_bwd_kernel<3>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
-        default: ERGM_LAUNCH(ln_bwd_kernel<4>, dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs); break;
+#define LN_BWD_LAUNCH(NV, B)                                                                                     \
+    do {                                                                                                         \
+        if (ln_bwd_rpw() == 2)                                                                                   \
+            ERGM_LAUNCH((ln_bwd_kernel<NV, B, 2>), dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd,   \
+                        gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs);                \
+        else                                                                                                     \
+            ERGM_LAUNCH((ln_bwd_kernel<NV, B, 1>), dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd,   \
+                        gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs);                \
+    } while (0)
+    switch (cdiv(E, 256) * 2 + (dy_bf16 ? 1 : 0)) {
+        case 2: LN_BWD_LAUNCH(1, false); break;
+        case 3: LN_BWD_LAUNCH(1, true); break;
+        case 4: LN_BWD_LAUNCH(2, false); break;
+        case 5: LN_BWD_LAUNCH(2, true); break;
+        case 6: LN_BWD_LAUNCH(3, false); break;
+        case 7: LN_BWD_LAUNCH(3, true); break;
+        case 8: LN_BWD_LAUNCH(4, false); break;
+        default: LN_BWD_LAUNCH(4, true); break;
     }
+#undef LN_BWD_LAUNCH
     return check_launch("layernorm_bwd");
 }
 
@@ -482,7 +514,7 @@ extern "C" int ergm_layernorm_bwd(const float* dy, const float* x, const float* 
     float* pg = reinterpret_cast<float*>(ws);
     float* pb = pg + (size_t)nb * E;
     hipStream_t s = as_stream(stream);
-    ERGM_TRY(layernorm_bwd_main(dy, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E), 0,
+    ERGM_TRY(layernorm_bwd_main(dy, 0, x, mean, rstd, gamma, dres, dres_bf16, pg, pb, rows, E, s, drop_site_of(dropout, E), 0,
                                  nullptr, nullptr, 0));
     return layernorm_param_reduce(pg, pb, rows, E, dgamma, dbeta, s);
 }
