@@ -10,6 +10,9 @@
 namespace ergm {
 
 constexpr int LN_WAVES_BWD = 8;  // one row per wave: 8 waves per CU in flight at T = 2048
+// rows per workgroup: one per wave (two per wave, 128 workgroups at T = 2048, halves the partials the dγ/dβ reduce
+// reads but cost +0.8 % at C2 and +3.7 % at C5: profiles/r05_experiments.txt #13)
+constexpr int LN_ROWS_PER_BLOCK_BWD = 8;
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // keep bits recomputed, common.h drop_keep4).
 // DYB: dy is the bf16 output of the data-gradient GEMM (the per-block LayerNorms), else f32 (ln_f: the LM-head
 // and emotion-head gradients summed in f32).
-template <int NV, bool DYB, int RPW>
+template <int NV, bool DYB>
 __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const void* __restrict__ dy_, const float* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, float* __restrict__ dres,
@@ -132,7 +135,8 @@ __global__ __launch_bounds__(64 * LN_WAVES_BWD) void ln_bwd_kernel(const void* _
     const float inv_e = 1.0f / (float)E;
     // each wave owns RPW rows and issues every load of all of them (x, dy and the residual gradient it
     // adds into) before the first reduction, so the HBM latency is paid once
-    const int r0 = (blockIdx.x * LN_WAVES_BWD + wave) * RPW;
+    constexpr int RPW = LN_ROWS_PER_BLOCK_BWD / LN_WAVES_BWD;
+    const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK_BWD + wave * RPW;
     float4 xh[RPW][NV], d[RPW][NV], o[RPW][NV];
     float mu[RPW], rs[RPW];
 #pragma unroll
@@ -441,15 +445,7 @@ namespace ergm {
 // Main LayerNorm-backward pass only: dres += dx, dres_bf16, and per-block dγ/dβ partials
 // (part_g/part_b: ln_bwd_nparts(rows) x E floats each), reduced later by layernorm_param_reduce.
 // drop_res: the updated dres is final and itself goes through `drop` (dres_bf16 then gets the same values).
-// Rows per workgroup: LN_WAVES_BWD waves of ln_bwd_rpw() rows each (ERGM_LN_RPW = 1 or 2).
-static int ln_bwd_rpw() {
-    static const int r = [] {
-        const char* e = getenv("ERGM_LN_RPW");
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
-    return r;
-}
-int ln_bwd_rows_per_part() { return LN_WAVES_BWD * ln_bwd_rpw(); }
+int ln_bwd_rows_per_part() { return LN_ROWS_PER_BLOCK_BWD; }
 int ln_bwd_nparts(int rows) { return cdiv(rows, ln_bwd_rows_per_part()); }
 
 int layernorm_bwd_main(const void* dy, int dy_bf16, const float* x, const float* mean, const float* rstd,
@@ -463,14 +459,8 @@ int layernorm_bwd_main(const void* dy, int dy_bf16, const float* x, const float*
     const int nb = ln_bwd_nparts(rows);
     auto* db = reinterpret_cast<__bf16*>(dres_bf16);
 #define LN_BWD_LAUNCH(NV, B)                                                                                     \
-    do {                                                                                                         \
-        if (ln_bwd_rpw() == 2)                                                                                   \
-            ERGM_LAUNCH((ln_bwd_kernel<NV, B, 2>), dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd,   \
-                        gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs);                \
-        else                                                                                                     \
-            ERGM_LAUNCH((ln_bwd_kernel<NV, B, 1>), dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd,   \
-                        gamma, dres, db, part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs);                \
-    } while (0)
+    ERGM_LAUNCH((ln_bwd_kernel<NV, B>), dim3(nb), dim3(64 * LN_WAVES_BWD), 0, s, dy, x, mean, rstd, gamma, dres, db,   \
+                part_g, part_b, rows, E, drop, drop_res, q8, qs, ld_qs)
     switch (cdiv(E, 256) * 2 + (dy_bf16 ? 1 : 0)) {
         case 2: LN_BWD_LAUNCH(1, false); break;
         case 3: LN_BWD_LAUNCH(1, true); break;

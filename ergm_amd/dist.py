@@ -53,6 +53,7 @@ class DPSync:
     def __init__(self, process_group=None, buckets: Optional[List[Tuple[int, int]]] = None,
                  grad_comm: Optional[str] = None):
         self.pg = process_group
+        self._wr_cache: Optional[Tuple[int, int]] = None
         self.buckets = buckets or []
         self._works: List = []
         self._stream = None
@@ -63,6 +64,8 @@ class DPSync:
             raise ValueError(f"grad_comm must be 'bf16' or 'fp32' (got {self.grad_comm!r})")
         self._pool = None          # bf16 exchange buffers, reused in stream order by every reduction
         self._pool32 = None        # fp32 gather buffer (consolidate_)
+        self._cur = None           # inside enqueue's fn: the side stream's handle (c_void_p)
+        self._coll = None          # (process group, all-to-all options, all-gather options) of the CUDA exchange
         self.bytes_per_step = 0    # gradient bytes this rank sent in the last backward (bench report)
         self.zero = self.grad_comm == "bf16" and os.environ.get("ERGM_DP_ZERO", "0") == "1"
         # consecutive block buckets exchanged together (ERGM_DP_MERGE, default 2): every exchange costs the
@@ -126,19 +129,24 @@ class DPSync:
             dist.all_reduce(vals, group=self.pg)
         self._master[idx] = vals
 
+    def _wr(self) -> Tuple[int, int]:
+        # (world, rank) of the group, fixed for its lifetime: asked ~60 times per step by the exchange, and
+        # dist.get_world_size / get_rank cost a few microseconds of Python each
+        if self._wr_cache is None:
+            if self.pg is None:
+                self._wr_cache = (1, 0)
+            else:
+                import torch.distributed as dist
+                self._wr_cache = (dist.get_world_size(self.pg), dist.get_rank(self.pg))
+        return self._wr_cache
+
     @property
     def world(self) -> int:
-        if self.pg is None:
-            return 1
-        import torch.distributed as dist
-        return dist.get_world_size(self.pg)
+        return self._wr()[0]
 
     @property
     def rank(self) -> int:
-        if self.pg is None:
-            return 0
-        import torch.distributed as dist
-        return dist.get_rank(self.pg)
+        return self._wr()[1]
 
     @property
     def active(self) -> bool:
@@ -181,6 +189,26 @@ class DPSync:
         c, r = self.chunk(n), self.rank
         return min(r * c, n), min((r + 1) * c, n)
 
+    def _group(self):
+        if self._coll is None:
+            from torch.distributed.distributed_c10d import AllgatherOptions, AllToAllOptions, _get_default_group
+            o1, o2 = AllToAllOptions(), AllgatherOptions()
+            o1.asyncOp = o2.asyncOp = True
+            self._coll = (self.pg or _get_default_group(), o1, o2)
+        return self._coll
+
+    def _a2a(self, recv: torch.Tensor, send: torch.Tensor) -> None:
+        """Equal-split all-to-all of CUDA buffers, the current stream ordered behind it (no host wait): the
+        process group's own call, which all_to_all_single makes after ~20 us of Python argument checks and
+        logging per call — 14 collectives per step under ZeRO-1 (verdict r04 #6)."""
+        g, o, _ = self._group()
+        g.alltoall_base(recv, send, [], [], o).wait()
+
+    def _ag(self, gath: torch.Tensor, mine: torch.Tensor) -> None:
+        """All-gather of equal CUDA chunks into ``gath`` (the process group's own call, as _a2a)."""
+        g, _, o = self._group()
+        g._allgather_base(gath, mine, o).wait()
+
     def _exchange(self, t: torch.Tensor):
         """bf16 all-to-all of t's chunks + the fp32 sum of this rank's chunk over ranks (rounded once to
         bf16): returns (mine, chunk, gath) with `mine` = this rank's reduced chunk, a view of `gath`."""
@@ -196,7 +224,7 @@ class DPSync:
             if W * chunk > n:
                 send[n:].zero_()
             L.call("ergm_cast_bf16", C.c_void_p(t.data_ptr()), C.c_void_p(send.data_ptr()), n, st)
-            dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+            self._a2a(recv, send)
             L.call("ergm_chunk_sum_bf16", C.c_void_p(recv.data_ptr()), W, chunk, C.c_void_p(mine.data_ptr()), st)
         else:  # gloo on CPU tensors (host-logic tests): the same arithmetic with torch ops
             send.zero_()
@@ -209,7 +237,7 @@ class DPSync:
         import torch.distributed as dist
         self.bytes_per_step += (self.world - 1) * mine.numel() * mine.element_size()
         if gath.is_cuda:
-            dist.all_gather_into_tensor(gath, mine, group=self.pg, async_op=True).wait()
+            self._ag(gath, mine)
         else:
             dist.all_gather_into_tensor(gath, mine.clone(), group=self.pg)
 
@@ -243,7 +271,6 @@ class DPSync:
         the rest of t keeps the local gradient."""
         lo, hi = self.shard(t.numel())
         if t.is_cuda:  # cast + all-to-all, then ONE kernel: rank-order sum, bf16 rounding, widened into t[lo:hi]
-            import torch.distributed as dist
             from . import _lib as L
             W, n = self.world, t.numel()
             chunk = self.chunk(n)
@@ -253,7 +280,7 @@ class DPSync:
             if W * chunk > n:
                 send[n:].zero_()
             L.call("ergm_cast_bf16", C.c_void_p(t.data_ptr()), C.c_void_p(send.data_ptr()), n, st)
-            dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+            self._a2a(recv, send)
             L.call("ergm_chunk_sum_bf16_f32", C.c_void_p(recv.data_ptr()), W, chunk, hi - lo,
                    C.c_void_p(t.data_ptr() + 4 * lo), st)
             return lo, hi
@@ -316,17 +343,16 @@ class DPSync:
         zero padding) -> all-to-all -> rank-order sum + this rank's AdamW shard + its bf16 all-gather slot
         (ergm_dp_sum_adamw, bitwise the chunk sum then ergm_adamw_step) -> all-gather -> shadow copy.  The numbers
         are those of reduce_scatter_ + post + _gather."""
-        import torch.distributed as dist
         from . import _lib as L
         W, n = self.world, b - a
         chunk = self.chunk(n)
         lo, hi = self.shard(n)
         send, recv, gath = self._buffers(chunk, grad.device)
         mine = gath.view(W, chunk)[self.rank]
-        st = C.c_void_p(torch.cuda.current_stream(grad.device).cuda_stream)
+        st = self._cur if self._cur is not None else C.c_void_p(torch.cuda.current_stream(grad.device).cuda_stream)
         g0 = grad.data_ptr()
         L.call("ergm_dp_pack_bf16", C.c_void_p(g0 + 4 * a), n, C.c_void_p(send.data_ptr()), W * chunk, st)
-        dist.all_to_all_single(recv, send, group=self.pg, async_op=True).wait()
+        self._a2a(recv, send)
         if hi > lo:
             o = 4 * (a + lo)
             L.call("ergm_dp_sum_adamw", C.c_void_p(recv.data_ptr()), W, chunk, hi - lo, C.c_void_p(g0 + o),
@@ -334,7 +360,7 @@ class DPSync:
                    C.c_void_p(nat["v"].data_ptr() + o), C.c_void_p(mine.data_ptr()), nat["lr"], nat["beta1"],
                    nat["beta2"], nat["eps"], nat["weight_decay"], nat["step_size"], nat["bc2_sqrt"], st)
         self.bytes_per_step += 2 * (W - 1) * chunk * 2
-        dist.all_gather_into_tensor(gath, mine, group=self.pg, async_op=True).wait()
+        self._ag(gath, mine)
         shadow[a:b].copy_(gath[:n])
         if self._master is not None:
             self._pend_master.append((a, b, lo, hi))
@@ -378,7 +404,11 @@ class DPSync:
         if wait is not None:
             wait(side.cuda_stream)
         with torch.cuda.stream(side):
-            fn()
+            self._cur = C.c_void_p(side.cuda_stream)  # the native calls' stream inside fn (no current_stream query)
+            try:
+                fn()
+            finally:
+                self._cur = None
 
     def bucket_ready(self, k: int, grad: torch.Tensor, post=None, wait=None, shadow=None) -> None:
         """Bucket k of the flat gradient buffer `grad` is final on the current stream: start its

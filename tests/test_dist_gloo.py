@@ -241,3 +241,33 @@ def test_bf16_exchange_trajectory_stays_within_bound_of_fp32():
     dl = max(abs(a - b) / abs(a) for a, b in zip(l32, l16))
     dp = ((p16 - p32).norm() / (p32 - r["p0"]).norm()).item()
     assert dl <= 1e-3 and dp <= 2e-2, (dl, dp)
+
+
+def _coll_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dp = DPSync(dist.group.WORLD)
+    assert (dp.world, dp.rank) == (world, rank)
+    c = 5
+    send = torch.arange(world * c, dtype=torch.float32) + 1000 * rank
+    recv = torch.empty_like(send)
+    dp._a2a(recv, send)  # the process group's own all-to-all (the CUDA exchange's path)
+    ref = torch.empty_like(send)
+    dist.all_to_all_single(ref, send)
+    assert torch.equal(recv, ref)
+    mine = torch.full((c,), float(rank + 1))
+    gath = torch.empty(world * c)
+    dp._ag(gath, mine)
+    ref = torch.empty(world * c)
+    dist.all_gather_into_tensor(ref, mine)
+    assert torch.equal(gath, ref)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_direct_collectives_match_the_c10d_wrappers(world):
+    """DPSync._a2a / _ag (the process group's alltoall_base / _allgather_base, used by the CUDA exchange to skip
+    the c10d wrappers' per-call Python) move the same data as all_to_all_single / all_gather_into_tensor."""
+    mp.spawn(_coll_worker, args=(world, _free_port()), nprocs=world, join=True)
