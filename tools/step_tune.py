@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--splits", default="1")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     ap.add_argument("--candidates", default=None, help="comma-separated kCfgs indices (default: the built-in list)")
+    ap.add_argument("--shapes", default=None, help="comma-separated MxNxK shapes to tune (default: every traced shape)")
     args = ap.parse_args()
     from ergm_amd.config import ERGMConfig
     from ergm_amd.data import synthetic_batch
@@ -102,6 +103,9 @@ def main():
     n = lib.ergm_gemm_trace(0, buf, 256)
     shapes = [tuple(buf[i * 5:(i + 1) * 5]) for i in range(n)]
     shapes.sort(key=lambda t: -2.0 * t[0] * t[1] * t[2])
+    if args.shapes:
+        want = {tuple(int(x) for x in w.split("x")) for w in args.shapes.split(",")}
+        shapes = [t for t in shapes if t[:3] in want]
     shapes = shapes[:args.max_shapes]
     for _ in range(10):
         step()
