@@ -1064,7 +1064,10 @@ static constexpr GemmOverride kStepTuned[] = {
     {2048, 768, 3072, ERGM_MK, ERGM_NK, 8, 1},   // c_fc data gradient
     {2048, 768, 2304, ERGM_MK, ERGM_NK, 15, 1},  // c_attn data gradient (cfg 8 until round 4's re-tune)
     {769, 3072, 2048, ERGM_KM, ERGM_KN, 15, 1},  // c_fc weight gradient (+ the bias row; round 4)
-    {769, 768, 2048, ERGM_KM, ERGM_KN, 11, 1},   // attn c_proj / q / cross c_proj weight gradients (round 4)
+    {769, 768, 2048, ERGM_KM, ERGM_KN, 16, 1},   // attn c_proj / q / cross c_proj weight gradients: the warp-
+                                                 // specialised 64 x 64 tile, launched singly (round 5's pass over the
+                                                 // KS2 / IL / warp-specialised configurations: -0.6 %, profiles/
+                                                 // r05_experiments.txt #16; cfg 11 in pairs since round 4)
     {1025, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1}, // GPT-2-medium attention c_proj weight gradient (C5)
     {1024, 1024, 4096, ERGM_KM, ERGM_KN, 15, 1},
     // config 5 (GPT-2-medium, B=32, T=4096) data gradients, round 5's re-tune on the current build (tools/step_tune.py

@@ -12,6 +12,7 @@ from ergm_amd.dataset import DialogueDataset, PadCollate
 from ergm_amd.model import GPT2LMHeadModel
 from ergm_amd.optim import FusedAdamW, get_polynomial_decay_schedule_with_warmup
 from ergm_amd.train import Trainer
+from _bitwise import assert_bitwise
 
 pytestmark = pytest.mark.gpu
 V, E = 500, 128
@@ -51,6 +52,17 @@ def _loader(ds):
     return torch.utils.data.DataLoader(ds, batch_size=4, shuffle=False, collate_fn=PadCollate(EOS, pad_multiple=16))
 
 
+def _state(model, opt):
+    st = opt.state[model.flat]
+    return {"master": model.flat.detach().clone(), "shadow": model.flat_b16.clone(),
+            "exp_avg": st["exp_avg"].clone(), "exp_avg_sq": st["exp_avg_sq"].clone()}
+
+
+def _same(a, b, what, layout):
+    for k in a:
+        assert_bitwise(b[k], a[k], f"{what}: {k}", layout)
+
+
 def test_trainer_epochs_checkpoint_and_resume(gpu):
     train_ds, valid_ds = _data(8, 1), _data(3, 2)
     tmp = tempfile.mkdtemp()
@@ -62,6 +74,7 @@ def test_trainer_epochs_checkpoint_and_resume(gpu):
     tr, va = t1.train(_loader(train_ds), _loader(valid_ds), 2, log=stats.append)
     assert tr.steps == 6 and tr.samples == len(train_ds) and va.samples == len(valid_ds)
     assert all(map(torch.isfinite, torch.tensor([tr.loss, va.loss])))
+    after2 = _state(m1, o1)  # the uninterrupted run after two epochs (localises a divergence below)
     first = t1.train_epoch(_loader(train_ds))
     ckpts = [f for f in os.listdir(tmp) if f.startswith("best_ckpt_epoch=")]
     assert ckpts, stats
@@ -72,6 +85,8 @@ def test_trainer_epochs_checkpoint_and_resume(gpu):
     m2, o2, s2 = _setup(gpu)
     t_mid = Trainer(m2, o2, s2)
     t_mid.train(_loader(train_ds), _loader(valid_ds), 2, log=lambda *_: None)
+    torch.cuda.synchronize()
+    _same(after2, _state(m2, o2), "second run vs the uninterrupted run after two epochs", m1.layout)
     path = os.path.join(tmp, "mid.ckpt")
     t_mid.save(path)
     m3, o3, s3 = _setup(gpu)
@@ -80,7 +95,7 @@ def test_trainer_epochs_checkpoint_and_resume(gpu):
     assert t3.last_epoch == 2
     again = t3.train_epoch(_loader(train_ds))
     torch.cuda.synchronize()
-    assert torch.equal(m3.flat, m1.flat)
+    assert_bitwise(m3.flat, m1.flat, "resumed third epoch vs the uninterrupted run: master", m1.layout)
     assert again.loss == first.loss and again.acc == first.acc
     assert va.loss < v0.loss  # training reduced the validation loss
 
