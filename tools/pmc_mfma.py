@@ -68,7 +68,7 @@ def main():
         from bench import lmhead_split_cols
         alg = 2.0 * 2048 * lmhead_split_cols(2048, 50304) * 768  # the main launch (bench's roofline kernel)
         out["lm_head_fwd"] = dict(rec, algorithmic_flops=alg, counted_over_algorithmic=rec["bf16_flops_counted"] / alg)
-    dw = [e for e in rows if (("gemm_pipe_kernel<" in e["name"] and ", true, true, " in e["name"]) or
+    dw = [e for e in rows if ((("gemm_pipe_kernel<" in e["name"] or "gemm_ws_kernel<" in e["name"]) and ", true, true, " in e["name"]) or
                               "gemm_dw2_kernel<" in e["name"]) and e["gui"] > 0]  # single and grouped launches
     if dw:
         out["dw_class"] = {"dispatches": len(dw),

@@ -71,7 +71,7 @@ def main():
                               "algorithmic_bytes": alg, "ratio": (fb + wb) / alg}
     # the weight-gradient GEMM class (bench.py's roofline): every KM x KN pipelined GEMM dispatch; mean
     # bytes per launch over the class against the mean algorithmic bytes of its C2 launches
-    dwk = [k for k in fetch if ("gemm_pipe_kernel<" in k and ", true, true, " in k) or "gemm_dw2_kernel<" in k]
+    dwk = [k for k in fetch if (("gemm_pipe_kernel<" in k or "gemm_ws_kernel<" in k) and ", true, true, " in k) or "gemm_dw2_kernel<" in k]
     if dwk:
         F, L = 4 * E, cfg.n_layer
         shapes = [(Vp, E)] + [(F + 1, E), (E + 1, F), (E + 1, E), (E + 1, E), (E + 1, E), (E + 1, 3 * E)] * L + \
