@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 9  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 10  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -79,6 +79,7 @@ _SIGS = {
     "ergm_gemm": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, sz, vp]),
     "ergm_gemm_f8": (i32, [C.POINTER(GemmDesc), vp, vp, vp, vp, vp, vp]),
     "ergm_gemm_f8_tune": (i32, [i32]),
+    "ergm_gemm_f8_set_override": (i32, [i32, i32, i32, i32]),
     "ergm_quant_rows_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp]),
     "ergm_quant_weight_fp8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp]),
     "ergm_gemm_mx": (i32, [C.POINTER(GemmDesc), vp, vp, i32, vp, vp, i32, vp, vp, vp, i32, i32, vp]),

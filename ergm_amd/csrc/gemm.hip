@@ -1348,8 +1348,29 @@ static void launch_f8(const GemmArgs& a, int cfg, hipStream_t s) {
     }
 }
 
-static int plan_f8(int M, int N) {
+// Per-shape overrides of the fp8 / MX tile configuration (ergm_gemm_f8_set_override: the in-step tuner) and the
+// built-in entries it measured; keyed on (M, N, K).
+struct F8Override {
+    int M, N, K, cfg;
+};
+static constexpr int kMaxF8Overrides = 32;
+static F8Override g_f8_over[kMaxF8Overrides];
+static int g_n_f8_over = 0;
+static constexpr F8Override kF8StepTuned[] = {
+    // config 5 (GPT-2-medium, B=32, S=128; forward chains of M = 2048): the MX c_fc GEMM on the 256 x 256 tile
+    // (tools/step_tune.py --config c5 --f8: 21.06 -> 20.85 ms/step, profiles/r05_step_tune_c5_f8.txt)
+    {2048, 4096, 1024, 3},
+};
+
+static int plan_f8(int M, int N, int K) {
     if (g_force_f8_cfg >= 0) return g_force_f8_cfg;
+    {
+        std::lock_guard<std::mutex> lk(g_over_mu);
+        for (int i = 0; i < g_n_f8_over; ++i)
+            if (g_f8_over[i].M == M && g_f8_over[i].N == N && g_f8_over[i].K == K) return g_f8_over[i].cfg;
+    }
+    for (const F8Override& o : kF8StepTuned)
+        if (o.cfg >= 0 && o.M == M && o.N == N && o.K == K) return o.cfg;
     const long t128 = tiles_of(M, N, 128, 128);
     if (t128 >= 4000) return 3;
     if (t128 >= 512) return 1;
@@ -1409,7 +1430,12 @@ extern "C" int ergm_gemm_mx(const ergm_gemm_desc* d, const void* A, const void* 
     ERGM_CHECK_ARG(!q_out || (q_scale && (e == ERGM_EPI_BIAS_GELU || e == ERGM_EPI_GELU_BWD) && d->N % 32 == 0 &&
                               ld_q >= d->N && ld_q % 8 == 0 && ld_qs >= d->M),
                    "ergm_gemm_mx: the MX copy of C needs a GELU / GELU' epilogue, N % 32 == 0 and its buffers");
-    const int cfg = plan_f8(d->M, d->N);
+    {  // the shape trace lists the fp8 / MX GEMMs with a_layout 16 (ergm_gemm_f8_set_override's keys)
+        ergm_gemm_desc t = *d;
+        t.a_layout = 16;
+        trace_shape(&t);
+    }
+    const int cfg = plan_f8(d->M, d->N, d->K);
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.A = reinterpret_cast<const __bf16*>(A);
@@ -1454,6 +1480,22 @@ extern "C" int ergm_gemm_mx(const ergm_gemm_desc* d, const void* A, const void* 
     return check_launch("ergm_gemm_mx");
 }
 
+extern "C" int ergm_gemm_f8_set_override(int M, int N, int K, int cfg) {
+    using namespace ergm;
+    ERGM_CHECK_ARG(cfg >= -1 && cfg < kNumF8Cfgs, "gemm_f8_set_override: cfg in [-1, %d)", kNumF8Cfgs);
+    std::lock_guard<std::mutex> lk(g_over_mu);
+    for (int i = 0; i < g_n_f8_over; ++i)
+        if (g_f8_over[i].M == M && g_f8_over[i].N == N && g_f8_over[i].K == K) {
+            if (cfg < 0) g_f8_over[i] = g_f8_over[--g_n_f8_over];
+            else g_f8_over[i].cfg = cfg;
+            return ERGM_OK;
+        }
+    if (cfg < 0) return ERGM_OK;
+    ERGM_CHECK_ARG(g_n_f8_over < kMaxF8Overrides, "gemm_f8_set_override: table full");
+    g_f8_over[g_n_f8_over++] = F8Override{M, N, K, cfg};
+    return ERGM_OK;
+}
+
 extern "C" int ergm_gemm_f8_tune(int cfg) {
     ERGM_CHECK_ARG(cfg >= -1 && cfg < ergm::kNumF8Cfgs, "gemm_f8_tune: cfg in [-1, %d)", ergm::kNumF8Cfgs);
     ergm::g_force_f8_cfg = cfg;
@@ -1480,7 +1522,12 @@ extern "C" int ergm_gemm_f8(const ergm_gemm_desc* d, const void* A, const float*
                    "ergm_gemm_f8: epilogue %d with c_dtype %d not supported", e, d->c_dtype);
     ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_RESID || (d->aux && d->ld_aux % 8 == 0), "ergm_gemm_f8: residual needs aux");
     ERGM_CHECK_ARG(e != ERGM_EPI_BIAS_GELU || (d->aux_out && d->ld_aux_out % 8 == 0), "ergm_gemm_f8: GELU needs aux_out");
-    const int cfg = plan_f8(d->M, d->N);
+    {  // the shape trace lists the fp8 / MX GEMMs with a_layout 16 (ergm_gemm_f8_set_override's keys)
+        ergm_gemm_desc t = *d;
+        t.a_layout = 16;
+        trace_shape(&t);
+    }
+    const int cfg = plan_f8(d->M, d->N, d->K);
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.A = reinterpret_cast<const __bf16*>(A);

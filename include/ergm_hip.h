@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 9
+#define ERGM_ABI_VERSION 10
 
 typedef enum {
     ERGM_OK = 0,
@@ -152,6 +152,10 @@ int ergm_gemm(const ergm_gemm_desc* desc, const void* A, const void* B, void* C,
 int ergm_gemm_f8(const ergm_gemm_desc* desc, const void* A, const float* a_scale, const void* B,
                  const float* b_scale, void* C, void* stream);
 int ergm_gemm_f8_tune(int cfg);
+/* Per-shape tile configuration of the fp8 / MX GEMMs (ergm_gemm_f8, ergm_gemm_mx) keyed on (M, N, K): the in-step
+ * tuner's hook (tools/step_tune.py --f8), as ergm_gemm_set_override is for the bf16 GEMMs; cfg -1 removes the entry.
+ * ergm_gemm_trace lists these GEMMs with a_layout 16.  ABI 10. */
+int ergm_gemm_f8_set_override(int M, int N, int K, int cfg);
 /* Row-wise e4m3 quantisation (activations): scale[r] = max_c |X[r][c]| / 448 (1 for a zero row),
  * Q[r][c] = e4m3(clamp(X[r][c] / scale[r], ±448)).  X bf16 or f32 (x_dtype), cols % 8 == 0.       */
 int ergm_quant_rows_fp8(const void* X, int x_dtype, int ldx, int rows, int cols, void* Q, int ldq,

@@ -7,6 +7,7 @@ configurations through ergm_gemm_set_override, keeping one only if the measured 
 more than the noise threshold (and again on a confirming re-measurement).
 
     python tools/step_tune.py [--config c2|c4|c5] [--steps 30] [--splits 1,2,4] [--out gpurun_out/step_tune.json]
+    python tools/step_tune.py --config c5 --f8      # the fp8 / MX GEMMs' tiles (ergm_gemm_f8_set_override)
 
 Split-K candidates (--splits) use the plan's scratch for their slab; a split that does not fit is
 reported by the GEMM as an error and skipped.
@@ -27,6 +28,7 @@ import bench  # noqa: E402
 from ergm_amd import _lib as L  # noqa: E402
 
 CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13, 22, 23, 24]  # kCfgs indices (gemm.hip)
+F8_TILE = {0: (128, 128), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (64, 64)}  # kF8Cfgs (gemm.hip)
 TILE = {0: (64, 64), 1: (128, 128), 2: (128, 128), 3: (128, 128), 4: (256, 128), 6: (256, 256), 7: (128, 64),
         8: (64, 128), 9: (256, 128), 10: (128, 128), 11: (64, 64), 12: (128, 64), 13: (64, 128), 14: (128, 128),
         15: (128, 128), 16: (64, 64), 17: (64, 64), 18: (128, 64), 19: (64, 128), 20: (128, 128), 21: (128, 128),
@@ -44,6 +46,7 @@ def main():
     ap.add_argument("--splits", default="1")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     ap.add_argument("--candidates", default=None, help="comma-separated kCfgs indices (default: the built-in list)")
+    ap.add_argument("--f8", action="store_true", help="tune the fp8 / MX GEMMs (traced with a_layout 16) instead")
     ap.add_argument("--shapes", default=None, help="comma-separated MxNxK shapes to tune (default: every traced shape)")
     args = ap.parse_args()
     from ergm_amd.config import ERGMConfig
@@ -83,7 +86,10 @@ def main():
     def set_cfg(key, cfg_split):
         M, N, K, al, bl = key
         c, sp = cfg_split if cfg_split is not None else (-1, 1)
-        L.check(lib.ergm_gemm_set_override(M, N, K, al, bl, c, sp), "override")
+        if al == 16:  # an fp8 / MX GEMM
+            L.check(lib.ergm_gemm_f8_set_override(M, N, K, c), "f8 override")
+        else:
+            L.check(lib.ergm_gemm_set_override(M, N, K, al, bl, c, sp), "override")
 
     def ab(key, inc, cand, rounds=2):
         """Interleaved A/B/A/B step times of the incumbent and the candidate configuration."""
@@ -102,6 +108,7 @@ def main():
     buf = (C.c_int * (256 * 5))()
     n = lib.ergm_gemm_trace(0, buf, 256)
     shapes = [tuple(buf[i * 5:(i + 1) * 5]) for i in range(n)]
+    shapes = [t for t in shapes if (t[3] == 16) == args.f8]
     shapes.sort(key=lambda t: -2.0 * t[0] * t[1] * t[2])
     if args.shapes:
         want = {tuple(int(x) for x in w.split("x")) for w in args.shapes.split(",")}
@@ -116,9 +123,12 @@ def main():
         M, N, K, al, bl = key
         best = None  # None = the automatic choice
         splits = [int(x) for x in args.splits.split(",")]
-        cands = [int(x) for x in args.candidates.split(",")] if args.candidates else CANDIDATES
+        if args.f8:
+            splits = [1]
+        cands = [int(x) for x in args.candidates.split(",")] if args.candidates else \
+            (list(F8_TILE) if args.f8 else CANDIDATES)
         for c, sp in [(c, sp) for sp in splits for c in cands]:
-            bm, bn = TILE[c]
+            bm, bn = (F8_TILE if args.f8 else TILE)[c]
             tiles = -(-M // bm) * -(-N // bn)
             if tiles < 24 or tiles > 20000 or (sp > 1 and (K // sp < 512 or tiles * sp > 2048)):
                 continue
