@@ -98,23 +98,38 @@ __global__ __launch_bounds__(256) void axpy_kernel(const float4* __restrict__ x,
     }
 }
 
-// Row-selective AdamW over a [rows][row_len] block: row r is updated iff (flag[r] != 0) == select.
-// One workgroup per row (grid-stride): a skipped row costs one flag byte.
+// Row-selective AdamW over a [rows][row_len] block: row r is updated iff (flag[r] != 0) == select.  Flat over the
+// block's float4 groups like adamw_kernel (two per thread per iteration, non-temporal parameter / moment traffic, every
+// lane busy); a group of a skipped row costs its row's flag byte (L1 / L2-resident: a row is 192 groups at E = 768).
+// Round 4's one-workgroup-per-row form ran the 88 %-selected untouched-row pass at 4.9 TB/s (192 of 256 lanes, one
+// group per thread, cached parameter traffic).
 __global__ __launch_bounds__(256) void adamw_rows_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v,
-                                                         bf16x4* __restrict__ pb, int rows, int row4,
+                                                         bf16x4* __restrict__ pb, size_t n4, int row4,
                                                          const uint8_t* __restrict__ flag, int select, AdamScalars sc) {
-    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-        if ((flag[r] != 0) != (select != 0)) continue;
-        for (int c = threadIdx.x; c < row4; c += 256) {
-            const size_t i = (size_t)r * row4 + c;
-            float4 pp = p[i], gg = nt_load4(g + i), mm = m[i], vv = v[i];
-            bf16x4 o;
-            adamw_one(pp, gg, mm, vv, o, sc);
-            p[i] = pp;
-            m[i] = mm;
-            v[i] = vv;
-            if (pb) pb[i] = o;
+    const size_t stride = (size_t)gridDim.x * 256;
+    const bool want = select != 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += 2 * stride) {
+        const size_t i2 = i + stride;
+        const bool on0 = (flag[(unsigned)i / (unsigned)row4] != 0) == want;  // n4 < 2^32 (host check)
+        const bool on1 = i2 < n4 && (flag[(unsigned)i2 / (unsigned)row4] != 0) == want;
+        float4 p0, g0, m0, v0, p1, g1, m1, v1;
+        if (on0) { p0 = ld4<true>(p + i); g0 = nt_load4(g + i); m0 = ld4<true>(m + i); v0 = ld4<true>(v + i); }
+        if (on1) { p1 = ld4<true>(p + i2); g1 = nt_load4(g + i2); m1 = ld4<true>(m + i2); v1 = ld4<true>(v + i2); }
+        bf16x4 o0, o1;
+        if (on0) {
+            adamw_one(p0, g0, m0, v0, o0, sc);
+            st4<true>(p + i, p0);
+            st4<true>(m + i, m0);
+            st4<true>(v + i, v0);
+            if (pb) pb[i] = o0;
+        }
+        if (on1) {
+            adamw_one(p1, g1, m1, v1, o1, sc);
+            st4<true>(p + i2, p1);
+            st4<true>(m + i2, m1);
+            st4<true>(v + i2, v1);
+            if (pb) pb[i2] = o1;
         }
     }
 }
@@ -169,10 +184,12 @@ extern "C" int ergm_adamw_rows(float* p, const float* g, float* m, float* v, voi
     ERGM_CHECK_ARG(!p_bf16 || (reinterpret_cast<uintptr_t>(p_bf16) & 7) == 0, "adamw_rows: bf16 copy alignment");
     if (rows == 0) return ERGM_OK;
     const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
-    unsigned grid = (unsigned)std::min(rows, 8192);
+    const size_t n4 = (size_t)rows * (row_len / 4);
+    ERGM_CHECK_ARG(n4 < ((size_t)1 << 32), "adamw_rows: block of %zu float4 groups too large", n4);
+    unsigned grid = grid_for2(n4);
     if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
     ERGM_LAUNCH(adamw_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (float4*)p, (const float4*)g,
-                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, rows, row_len / 4, (const uint8_t*)row_flag, select,
+                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, row_len / 4, (const uint8_t*)row_flag, select,
                        sc);
     return check_launch("adamw_rows");
 }
