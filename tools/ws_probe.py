@@ -1,6 +1,7 @@
 """Uninitialised-read probe of the executor workspace (GPU box): the trainer test's model and data (tests/
-test_gpu_train.py) trained two epochs three times, with every runner workspace pre-filled with 0x00, 0xFF (NaN
-for f32 / bf16) and 0x3F bytes before the plan is created; the three final states must be bitwise equal if no
+test_gpu_train.py) trained two epochs three times, with every runner allocation made through torch.empty (the
+executor workspace, the logits / emotion-logit / loss outputs of each forward) pre-filled with 0x00, 0xFF (NaN for
+f32 / bf16) and 0x3F bytes; the three final states must be bitwise equal if no
 kernel reads workspace bytes it has not written.  Usage: python tools/ws_probe.py"""
 import os
 import sys
@@ -22,8 +23,8 @@ proxy = types.SimpleNamespace(**{k: getattr(torch, k) for k in dir(torch) if not
 
 def _empty(*a, **k):
     t = torch.empty(*a, **k)
-    if FILL[0] is not None and k.get("dtype") == torch.uint8:
-        t.fill_(FILL[0])
+    if FILL[0] is not None:  # every torch.empty of the runner: the workspace (bytes) and the forward's outputs
+        t.view(torch.uint8).fill_(FILL[0]) if t.is_contiguous() and t.numel() else None
     return t
 
 
