@@ -110,6 +110,7 @@ struct ergm_model_plan {
     // dW GEMM over K+1 rows also yields the bias gradient (each bias is stored right after its weight).
     int XE, XF;
     bool fused_bias;  // the ones-column layout holds (every bias right after its weight): dW over M+1 rows
+    bool ones_pending;  // the ones columns are written by the first forward, on the caller's stream
     // activations
     float** resid;  // 3L+1 residual-stream tensors [T][E] f32
     std::vector<float*> resid_v;
@@ -791,8 +792,12 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->have_fwd = false;
     P->ln_pending = 0;
     // Fused bias gradients need every Conv1D bias stored right after its weight (ergm_amd/params.py lays the
-    // flat buffers out that way) and a ones column in the activations (set here; producers write columns
-    // < E / < F only); other layouts take the in-GEMM column sums (ergm_gemm_desc.bias_grad).
+    // flat buffers out that way) and a ones column in the activations (producers write columns < E / < F
+    // only); other layouts take the in-GEMM column sums (ergm_gemm_desc.bias_grad).  The first forward
+    // writes the ones columns on its own stream: the caller's allocator may hand over a workspace whose
+    // previous owner still has work queued on that stream, which a write from here (legacy null stream,
+    // unordered with non-blocking streams) would race — and lose the columns to (profiles/r05_experiments.txt #29).
+    P->ones_pending = true;
     {
         const int64_t E = d.n_embd, F = d.n_inner;
         const int64_t* o = P->p.layer_off;
@@ -801,19 +806,6 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
                         follows(ERGM_T_XQ_W, ERGM_T_XQ_B, E, E) && follows(ERGM_T_XPROJ_W, ERGM_T_XPROJ_B, E, E) &&
                         follows(ERGM_T_FC_W, ERGM_T_FC_B, E, F) && follows(ERGM_T_MPROJ_W, ERGM_T_MPROJ_B, F, E) &&
                         P->p.g_capkv_b == P->p.g_capkv_w + E * P->L2E;
-        int rc = ERGM_OK;
-        for (int l = 0; l < d.n_layer && rc == ERGM_OK; ++l) {
-            LayerActs& a = P->la[l];
-            const void* cols[5] = {a.ln1, a.lnx, a.ln2, a.ao, a.xo};
-            for (int i = 0; i < 5 && rc == ERGM_OK; ++i) rc = fill_ones_col((void*)cols[i], P->T, P->XE, d.n_embd, nullptr);
-            if (rc == ERGM_OK) rc = fill_ones_col(a.act, P->T, P->XF, d.n_inner, nullptr);
-        }
-        if (rc == ERGM_OK) rc = fill_ones_col(P->cap, P->T, P->XE, d.n_embd, nullptr);
-        if (rc == ERGM_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = fail(ERGM_EHIP, "model_create: sync");
-        if (rc != ERGM_OK) {
-            ergm_model_destroy(P);
-            return rc;
-        }
     }
     P->ids = P->tt = P->cap_ids = P->labels = P->emo_labels = nullptr;
     P->vis = P->aud = nullptr;
@@ -1268,7 +1260,19 @@ extern "C" int ergm_model_forward(ergm_model_plan* P, void* logits, float* emo_l
     ERGM_CHECK_ARG(!(P->labels || P->emo_labels) || out_loss, "model_forward: labels need out_loss");
     bind_clear();
     P->stage_pt = nullptr;  // a fork point is armed and taken inside one native call
-    return do_forward(P, logits, emo_logits, out_loss, train, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    if (P->ones_pending) {  // before any fork from s: every other stream of the step is ordered after these
+        const ergm_model_dims& d = P->d;
+        for (int l = 0; l < d.n_layer; ++l) {
+            LayerActs& a = P->la[l];
+            const void* cols[5] = {a.ln1, a.lnx, a.ln2, a.ao, a.xo};
+            for (int i = 0; i < 5; ++i) ERGM_TRY(fill_ones_col((void*)cols[i], P->T, P->XE, d.n_embd, s));
+            ERGM_TRY(fill_ones_col(a.act, P->T, P->XF, d.n_inner, s));
+        }
+        ERGM_TRY(fill_ones_col(P->cap, P->T, P->XE, d.n_embd, s));
+        P->ones_pending = false;
+    }
+    return do_forward(P, logits, emo_logits, out_loss, train, s);
 }
 
 namespace {

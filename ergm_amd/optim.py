@@ -230,6 +230,11 @@ class FusedAdamW(torch.optim.Optimizer):
                 r.dp.sharded.clear()
             return
         super().load_state_dict(state_dict)
+        # a checkpoint read with map_location=<gpu> (Trainer.load) puts the step count on the device, and every
+        # step's host read of it (the bias corrections) would then wait for the GPU: keep it on the host
+        for st in self.state.values():
+            if torch.is_tensor(st.get("step")) and st["step"].device.type != "cpu":
+                st["step"] = st["step"].detach().to("cpu", torch.float32)
 
     def state_dict(self):
         if self.model is not None:

@@ -93,6 +93,7 @@ def test_trainer_epochs_checkpoint_and_resume(gpu):
     t3 = Trainer(m3, o3, s3)
     t3.load(path)
     assert t3.last_epoch == 2
+    assert o3.state[m3.flat]["step"].device.type == "cpu"  # no per-step host wait on a device step count
     again = t3.train_epoch(_loader(train_ds))
     torch.cuda.synchronize()
     assert_bitwise(m3.flat, m1.flat, "resumed third epoch vs the uninterrupted run: master", m1.layout)
