@@ -1,0 +1,29 @@
+"""The trainer resume test (tests/test_gpu_train.py) repeated N times in one process (GPU box): each repetition's
+models die with it and are collected at some later point (the model and its overlapped optimizer reference each
+other), so later repetitions run beside that teardown.  ``--gc`` collects and synchronises before every repetition.
+Usage: python tools/resume_loop.py N [--gc]"""
+import gc
+import os
+import sys
+
+import torch
+
+here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, here)
+sys.path.insert(0, os.path.join(here, "tests"))
+from test_gpu_train import test_trainer_epochs_checkpoint_and_resume as resume_test  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+collect = "--gc" in sys.argv
+dev = torch.device("cuda:0")
+fails = 0
+for i in range(n):
+    if collect:
+        gc.collect()
+        torch.cuda.synchronize()
+    try:
+        resume_test(dev)
+    except AssertionError as ex:
+        fails += 1
+        print(f"repetition {i}: FAILED {str(ex)[:300]}", flush=True)
+print(f"{'gc' if collect else 'plain'}: {n - fails}/{n} passed", flush=True)
