@@ -1,7 +1,8 @@
 """The trainer resume test (tests/test_gpu_train.py) repeated N times in one process (GPU box): each repetition's
 models die with it and are collected at some later point (the model and its overlapped optimizer reference each
 other), so later repetitions run beside that teardown.  ``--gc`` collects and synchronises before every repetition.
-Usage: python tools/resume_loop.py N [--gc]"""
+``--warm S`` first runs S seconds of large GEMMs (the GPU's clocks and temperature after a test suite, no other
+state).  Usage: python tools/resume_loop.py N [--gc] [--warm S]"""
 import gc
 import os
 import sys
@@ -16,6 +17,16 @@ from test_gpu_train import test_trainer_epochs_checkpoint_and_resume as resume_t
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 collect = "--gc" in sys.argv
 dev = torch.device("cuda:0")
+if "--warm" in sys.argv:
+    import time
+    secs = float(sys.argv[sys.argv.index("--warm") + 1])
+    A = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    t0 = time.time()
+    while time.time() - t0 < secs:
+        for _ in range(50):
+            A.mm(A)
+        torch.cuda.synchronize()
+    print(f"warmed {secs:.0f} s", flush=True)
 fails = 0
 for i in range(n):
     if collect:
