@@ -2,7 +2,9 @@
 models die with it and are collected at some later point (the model and its overlapped optimizer reference each
 other), so later repetitions run beside that teardown.  ``--gc`` collects and synchronises before every repetition.
 ``--warm S`` first runs S seconds of large GEMMs (the GPU's clocks and temperature after a test suite, no other
-state).  Usage: python tools/resume_loop.py N [--gc] [--warm S]"""
+state).  ``--scribble`` fills the allocator's cached blocks with random values before every repetition (tensors of
+many sizes allocated, filled and freed), so memory a repetition reads without writing holds other values than the
+previous repetition left.  Usage: python tools/resume_loop.py N [--gc] [--warm S] [--scribble]"""
 import gc
 import os
 import sys
@@ -27,8 +29,15 @@ if "--warm" in sys.argv:
             A.mm(A)
         torch.cuda.synchronize()
     print(f"warmed {secs:.0f} s", flush=True)
+scribble = "--scribble" in sys.argv
+g = torch.Generator(device=dev).manual_seed(7)
 fails = 0
 for i in range(n):
+    if scribble:
+        junk = [torch.randn(int(k), device=dev, generator=g) for k in
+                torch.randint(1, 1 << 18, (400,), generator=torch.Generator().manual_seed(i)).tolist()]
+        junk += [torch.randn(1 << 22, device=dev, generator=g) for _ in range(8)]
+        del junk
     if collect:
         gc.collect()
         torch.cuda.synchronize()
@@ -37,4 +46,4 @@ for i in range(n):
     except AssertionError as ex:
         fails += 1
         print(f"repetition {i}: FAILED {str(ex)[:300]}", flush=True)
-print(f"{'gc' if collect else 'plain'}: {n - fails}/{n} passed", flush=True)
+print(f"{'gc' if collect else 'scribble' if scribble else 'plain'}: {n - fails}/{n} passed", flush=True)
