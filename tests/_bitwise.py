@@ -44,6 +44,9 @@ def describe(a: torch.Tensor, b: torch.Tensor, layout=None) -> str:
            f"({float(fa[first]):.9g} vs {float(fb[first]):.9g})")
     if layout is not None and a.numel() >= layout.total:
         msg += f" = {param_at(layout, first)}"
+        if n <= 64:  # a localised difference: every element (its pattern points at the kernel and tile)
+            msg += "; all: " + ", ".join(param_at(layout, int(i)).split(".")[-1] if k else param_at(layout, int(i))
+                                          for k, i in enumerate(ne.nonzero().reshape(-1).tolist()))
     return msg
 
 

@@ -45,5 +45,5 @@ for i in range(n):
         resume_test(dev)
     except AssertionError as ex:
         fails += 1
-        print(f"repetition {i}: FAILED {str(ex)[:300]}", flush=True)
+        print(f"repetition {i}: FAILED {str(ex)[:2500]}", flush=True)
 print(f"{'gc' if collect else 'scribble' if scribble else 'plain'}: {n - fails}/{n} passed", flush=True)
