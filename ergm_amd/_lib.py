@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libergm_hip.so")
 
-ABI_VERSION = 10  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
+ABI_VERSION = 11  # ERGM_ABI_VERSION of include/ergm_hip.h this binding matches
 ERGM_OK, ERGM_EINVAL, ERGM_EUNSUPPORTED, ERGM_EHIP = 0, -1, -2, -3
 F32, BF16 = 0, 1
 MK, KM = 0, 1
@@ -111,7 +111,7 @@ _SIGS = {
     "ergm_chunk_sum_bf16_f32": (i32, [vp, i32, sz, sz, vp, vp]),
     "ergm_cast_f32": (i32, [vp, vp, sz, vp]),
     "ergm_dp_pack_bf16": (i32, [vp, sz, vp, sz, vp]),
-    "ergm_dp_sum_adamw": (i32, [vp, i32, sz, sz, vp, vp, vp, vp, vp, f64, f64, f64, f32, f64, f32, f32, vp]),
+    "ergm_dp_sum_adamw": (i32, [vp, i32, sz, sz, vp, vp, vp, vp, vp, f64, f64, f64, f32, f64, f32, f32, i32, vp]),
     "ergm_model_workspace_size": (sz, [C.POINTER(ModelDims)]),
     "ergm_model_create": (i32, [C.POINTER(ModelDims), C.POINTER(ModelParams), vp, sz, C.POINTER(vp)]),
     "ergm_model_destroy": (i32, [vp]),

@@ -334,16 +334,19 @@ extern "C" int ergm_dp_pack_bf16(const float* src, size_t n, void* dst, size_t t
 
 extern "C" int ergm_dp_sum_adamw(const void* in, int nchunks, size_t chunk, size_t n, float* grad, float* p, float* m,
                                  float* v, void* shadow, double lr, double beta1, double beta2, float eps,
-                                 double weight_decay, float step_size, float bc2_sqrt, void* stream) {
+                                 double weight_decay, float step_size, float bc2_sqrt, int max_blocks, void* stream) {
     ERGM_CHECK_ARG(in && grad && p && m && v && shadow && nchunks > 0 && chunk % 4 == 0 && n % 4 == 0 && n <= chunk,
                    "dp_sum_adamw: bad argument");
+    ERGM_CHECK_ARG(max_blocks >= 0, "dp_sum_adamw: max_blocks must be >= 0");
     ERGM_CHECK_ARG(aligned16(grad) && aligned16(p) && aligned16(m) && aligned16(v) &&
                        (reinterpret_cast<uintptr_t>(shadow) & 7) == 0 && (reinterpret_cast<uintptr_t>(in) & 7) == 0,
                    "dp_sum_adamw: alignment");
     const size_t n4 = n / 4;
     if (n4 == 0) return ERGM_OK;
     const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
-    ERGM_LAUNCH(dp_sum_adamw_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), (const bf16x4*)in, nchunks,
+    unsigned grid = grid_for(n4);
+    if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
+    ERGM_LAUNCH(dp_sum_adamw_kernel, dim3(grid), dim3(256), 0, as_stream(stream), (const bf16x4*)in, nchunks,
                 chunk / 4, n4, (float4*)grad, (float4*)p, (float4*)m, (float4*)v, (bf16x4*)shadow, sc);
     return check_launch("dp_sum_adamw");
 }

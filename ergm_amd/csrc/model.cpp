@@ -173,6 +173,7 @@ struct ergm_model_plan {
     // backward scratch
     float *dh, *dy, *dcap, *delta;
     __bf16* dyb;  // the block LayerNorms' incoming gradient: their data-gradient GEMM's bf16 output (ln_f's: dy, f32)
+    bool ln_dy_f32;  // ERGM_LN_DY_F32=1: the block LayerNorms read an f32 data-gradient GEMM output (dy) instead
     __bf16 *d_o, *dkv_all;
     // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
     // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
@@ -609,9 +610,11 @@ int ln_bwd_rows(ergm_model_plan* P, hipStream_t s, const float* x, const float* 
     // itself goes through the embedding dropout (src/model.py:506), folded into this pass.
     const ergm_dropout dd = resid_drop(P, slot, r0 / P->d.seq);
     const int fin = slot == 0;
-    // the block LayerNorms read their data-gradient GEMM's bf16 output (as the reference's autocast GEMM backward
-    // hands LayerNorm a bf16 gradient); ln_f (slot 3L) the f32 sum of the LM-head and emotion-head gradients
-    const bool yb = slot != 3 * P->d.n_layer;
+    // the block LayerNorms read their data-gradient GEMM's output rounded to bf16 — a rounding the fp32 reference
+    // does not have (src/main.py trains without autocast), kept because it halves the LayerNorm backward's dy traffic
+    // (-0.3 % C2 step, profiles/r05_experiments.txt #11) at no measurable cost in the parity margins (DESIGN.md §10;
+    // ERGM_LN_DY_F32=1 keeps dy in f32); ln_f (slot 3L) reads the f32 sum of the LM-head and emotion-head gradients
+    const bool yb = slot != 3 * P->d.n_layer && !P->ln_dy_f32;
     return layernorm_bwd_main(yb ? (const void*)(P->dyb + o) : (const void*)(P->dy + o), yb, x + o, mean + r0, rstd + r0, gamma, P->dh + o, fin ? nullptr : dh_b + o,
                               pg + po, pb + po, rows, E, s, drop_site_of(&dd, E), fin, nullptr, nullptr, T);
 }
@@ -636,7 +639,9 @@ int ln_reduce_flush(ergm_model_plan* P, const Chains& ch) {
         hipEvent_t e = stream_point(P, ch.s[0], P->ev_fork);
         if (!e || hipStreamWaitEvent(P->side, e, 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream fork failed");
         for (int i = 1; i < ch.n; ++i) ERGM_TRY(fork_side(P, ch.s[i]));
-        P->stage_pt = e;  // the end of the stage on ch.s[0]: nothing more is enqueued there in this call
+        // the end of the stage on ch.s[0] (nothing more is enqueued there in this call) — unless a second chain's fork
+        // re-recorded ev_fork on fwd2 just now: then opt_wait records its own point on the caller's stream
+        P->stage_pt = ch.n == 1 ? e : nullptr;
     }
     const int n = P->ln_pending;
     P->ln_pending = 0;
@@ -764,6 +769,8 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     P->bwd_chains = 1;
     if (const char* e = getenv("ERGM_BWD_CHAINS")) P->bwd_chains = atoi(e);
     if (const char* e = getenv("ERGM_FP8_MX")) P->mx = atoi(e) != 0;
+    P->ln_dy_f32 = false;
+    if (const char* e = getenv("ERGM_LN_DY_F32")) P->ln_dy_f32 = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -1348,8 +1355,9 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     // per-chain row offset helper (dry run: pointers stay null)
     auto R = [&](auto* p, int c, size_t ld) { return (P->dry || !p) ? p : p + (size_t)ch.b0[c] * S * ld; };
     auto Tc = [&](int c) { return ch.nb[c] * S; };
-    // the block LayerNorms' incoming gradient (ln_bwd_rows reads the same buffer)
-    auto DYO = [&](int c) { return R(P->dyb, c, E); };
+    // the block LayerNorms' incoming gradient (ln_bwd_rows reads the same buffer): bf16, or f32 (ln_dy_f32)
+    auto DYO = [&](int c) { return P->ln_dy_f32 ? (void*)R(P->dy, c, E) : (void*)R(P->dyb, c, E); };
+    const int dyo_t = P->ln_dy_f32 ? ERGM_F32 : ERGM_BF16;
     // Weight-gradient pairs (mlp c_proj + c_fc, cross c_proj + q, attn c_proj + c_attn) are forked to the side
     // stream once the dY of the second member is formed.
     // fork points: with one data-gradient chain, the launch each weight-gradient fork waits for carries the
@@ -1365,7 +1373,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // mlp c_proj + c_fc weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, F, R(dpre, c, F), F, ERGM_MK, LB(P, l, ERGM_T_FC_W), F, ERGM_NK,
-                      DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
+                      DYO(c), E, dyo_t, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x2, a.m2, a.r2, LF(P, l, ERGM_T_LN2_W), dh2, 3 * l + 2, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 2, LG(P, l, ERGM_T_LN2_W), LG(P, l, ERGM_T_LN2_B)));
@@ -1403,7 +1411,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // cross c_proj + q weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, E, R(dxq, c, E), E, ERGM_MK, LB(P, l, ERGM_T_XQ_W), E, ERGM_NK,
-                      DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
+                      DYO(c), E, dyo_t, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x1, a.mx, a.rx, LF(P, l, ERGM_T_LNX_W), dh1, 3 * l + 1, ch.b0[c] * S, Tc(c)));
     ERGM_TRY(ln_reduce_add(P, 3 * l + 1, LG(P, l, ERGM_T_LNX_W), LG(P, l, ERGM_T_LNX_B)));
@@ -1441,7 +1449,7 @@ int do_backward_layer(ergm_model_plan* P, int l, hipStream_t s) {
     ERGM_TRY(dw_flush(P, ch));  // attn c_proj + c_attn weight gradients
     for (int c = 0; c < ch.n; ++c)
         ERGM_TRY(gemm(P, ch.s[c], Tc(c), E, 3 * E, R(dqkv, c, 3 * E), 3 * E, ERGM_MK, LB(P, l, ERGM_T_ATTN_W), 3 * E,
-                      ERGM_NK, DYO(c), E, ERGM_BF16, ERGM_EPI_NONE));
+                      ERGM_NK, DYO(c), E, dyo_t, ERGM_EPI_NONE));
     for (int c = 0; c < ch.n; ++c) {
         if (arm) arm_fork(P, s);  // ln_1's backward: the stage's last launch (LayerNorm reduce, optimizer)
         ERGM_TRY(ln_bwd_rows(P, ch.s[c], x0, a.m1, a.r1, LF(P, l, ERGM_T_LN1_W), dh0, 3 * l, ch.b0[c] * S, Tc(c)));

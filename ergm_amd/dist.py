@@ -358,7 +358,8 @@ class DPSync:
             L.call("ergm_dp_sum_adamw", C.c_void_p(recv.data_ptr()), W, chunk, hi - lo, C.c_void_p(g0 + o),
                    C.c_void_p(nat["p"].data_ptr() + o), C.c_void_p(nat["m"].data_ptr() + o),
                    C.c_void_p(nat["v"].data_ptr() + o), C.c_void_p(mine.data_ptr()), nat["lr"], nat["beta1"],
-                   nat["beta2"], nat["eps"], nat["weight_decay"], nat["step_size"], nat["bc2_sqrt"], st)
+                   nat["beta2"], nat["eps"], nat["weight_decay"], nat["step_size"], nat["bc2_sqrt"],
+                   int(nat.get("max_blocks", 0)), st)
         self.bytes_per_step += 2 * (W - 1) * chunk * 2
         self._ag(gath, mine)
         shadow[a:b].copy_(gath[:n])

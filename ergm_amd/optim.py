@@ -160,7 +160,7 @@ class FusedAdamW(torch.optim.Optimizer):
                                b2, eps, wd, t, nb)
         # what a fused native exchange (dist.DPSync, ergm_dp_sum_adamw) needs to apply the same update itself
         post.native = dict(p=flat.data, m=m, v=v, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
-                           step_size=lr / (1 - b1 ** t), bc2_sqrt=math.sqrt(1 - b2 ** t))
+                           step_size=lr / (1 - b1 ** t), bc2_sqrt=math.sqrt(1 - b2 ** t), max_blocks=nb)
         return post
 
     def _native_desc(self, flat, model):

@@ -49,6 +49,8 @@ class Trainer:
         self.ckpt_dir = ckpt_dir
         self.best_ppl = float("inf")
         self.last_epoch = 0
+        # called after every training step (after the optimizer and scheduler steps): diagnostics / tests
+        self.step_hook = None
 
     # ---- one pass -------------------------------------------------------------------------
     def _pass(self, loader: Iterable[Dict[str, torch.Tensor]], train: bool) -> EpochStats:
@@ -66,6 +68,8 @@ class Trainer:
                 self.optim.step()
                 if self.sched is not None:
                     self.sched.step()
+                if self.step_hook is not None:
+                    self.step_hook()
             else:
                 with torch.no_grad():
                     out = self.model(**kw)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ERGM_ABI_VERSION 10
+#define ERGM_ABI_VERSION 11  /* 11: ergm_dp_sum_adamw takes max_blocks */
 
 typedef enum {
     ERGM_OK = 0,
@@ -315,11 +315,12 @@ int ergm_chunk_sum_bf16_f32(const void* in, int nchunks, size_t chunk, size_t n,
  * issued two or three: ergm_dp_pack_bf16 casts a bucket's n fp32 gradients into the all-to-all send buffer and zeroes
  * its padding up to `total`; ergm_dp_sum_adamw sums the received chunks in rank order, rounds once to bf16 (the
  * ergm_chunk_sum_bf16_f32 value, bitwise), writes the widened sum into grad[0..n) and applies ergm_adamw_step's
- * update to p / m / v [0..n) with it, the updated bf16 parameters going to `shadow` (this rank's all-gather slot). */
+ * update to p / m / v [0..n) with it, the updated bf16 parameters going to `shadow` (this rank's all-gather slot);
+ * max_blocks > 0 caps its grid like ergm_adamw_step's (an update overlapped with the backward's GEMMs). */
 int ergm_dp_pack_bf16(const float* src, size_t n, void* dst, size_t total, void* stream);
 int ergm_dp_sum_adamw(const void* in, int nchunks, size_t chunk, size_t n, float* grad, float* p, float* m, float* v,
                       void* shadow, double lr, double beta1, double beta2, float eps, double weight_decay,
-                      float step_size, float bc2_sqrt, void* stream);
+                      float step_size, float bc2_sqrt, int max_blocks, void* stream);
 int ergm_cast_f32(const void* src, float* dst, size_t n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

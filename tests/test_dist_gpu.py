@@ -46,7 +46,8 @@ def _step(model, opt, batch, dev):
 def _worker(rank, world, port, out_path, mode="fp32"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["ERGM_DP_GRAD"] = "fp32" if mode == "fp32" else "bf16"
-    os.environ["ERGM_DP_ZERO"] = "1" if mode == "bf16" else "0"
+    os.environ["ERGM_DP_ZERO"] = "1" if mode in ("bf16", "bf16py") else "0"
+    os.environ["ERGM_DP_NATIVE"] = "0" if mode == "bf16py" else "1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from ergm_amd.model import GPT2LMHeadModel
@@ -104,21 +105,24 @@ def _run(mode):
 _RUNS = {}
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16nz", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "bf16nz", "bf16", "bf16py"])
 def test_dp2_fused_step_matches_single_process(gpu, mode):
     """Exchange precisions: "fp32" all-reduce (the default); "bf16nz" the bf16 all-to-all / fp32 chunk sum /
     all-gather (ergm_chunk_sum_bf16, ergm_cast_f32) with the replicated update; "bf16" the same exchange with
-    the sharded update (ZeRO-1, opt-in, the bench's choice) — bitwise the replicated one after consolidate_,
-    and until then model.state_dict() / FusedAdamW.state_dict() refuse (a rank-0 checkpoint
-    would mix trained and untrained chunks)."""
+    the sharded update (ZeRO-1, opt-in) — bitwise the replicated one after consolidate_, and until then
+    model.state_dict() / FusedAdamW.state_dict() refuse (a rank-0 checkpoint would mix trained and
+    untrained chunks); "bf16py" the sharded update through the Python sequence (ERGM_DP_NATIVE=0: reduce_scatter_ +
+    ergm_adamw_step + all-gather), bitwise the native ergm_dp_pack_bf16 / ergm_dp_sum_adamw bucket."""
     torch.cuda.synchronize()
     r, r1 = _RUNS[mode] = _run(mode)
-    assert r["sharded"] == (mode == "bf16") and r1["sharded"] == (mode == "bf16")
-    assert r["refused"] == [mode == "bf16"] * 2 and r1["refused"] == [mode == "bf16"] * 2 and r["sd_ok"]
-    if mode == "bf16" and "bf16nz" in _RUNS:
-        z = _RUNS["bf16nz"][0]
-        for k in ("grad", "flat", "m", "v", "shadow"):
-            assert torch.equal(r[k], z[k]), k
+    zero = mode in ("bf16", "bf16py")
+    assert r["sharded"] == zero and r1["sharded"] == zero
+    assert r["refused"] == [zero] * 2 and r1["refused"] == [zero] * 2 and r["sd_ok"]
+    for other in ("bf16nz", "bf16"):
+        if zero and other != mode and other in _RUNS:
+            z = _RUNS[other][0]
+            for k in ("grad", "flat", "m", "v", "shadow"):
+                assert torch.equal(r[k], z[k]), (other, k)
     # both ranks hold the same all-reduced gradient and took the same update
     assert torch.equal(r["grad"], r1["grad"]) and torch.equal(r["flat"], r1["flat"])
     err = ((r["grad"] - r["ref_grad"]).norm() / r["ref_grad"].norm()).item()
