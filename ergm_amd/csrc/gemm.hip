@@ -151,9 +151,11 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
 // global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
 // (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
 // the staging buffer is (BM/WGM)*(BN+4) floats.  slab != nullptr: raw f32 split-K partials.
+// MF: the accumulator fragments' MFMA shape — 16 (f32x4 per 16x16 fragment: lane l holds rows 4(l>>4)+r of column
+// l&15) or 32 (f32x16 per 32x32 fragment: lane l holds rows (r&3) + 8(r>>2) + 4(l>>5) of column l&31).
 template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN,
-          bool RS = false, bool QMX = false>
-__device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (&acc)[FM][FN], int m0, int n0,
+          bool RS = false, bool QMX = false, int MF = 16, typename AccT = f32x4>
+__device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, AccT (&acc)[FM][FN], int m0, int n0,
                                            float alpha, float* slab) {
     // NT: every thread of the workgroup (a warp-specialised kernel adds producer waves, which only
     // help with the copy-out; accumulator fragments come from the WGM x WGN consumer waves)
@@ -167,13 +169,24 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, f32x4 (
     for (int pass = 0; pass < WGM; ++pass) {
         __syncthreads();
         if (wave < WGM * WGN && wm == pass) {
+            if constexpr (MF == 16) {
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+                for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j)
+                    for (int j = 0; j < FN; ++j)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        t[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+                        for (int r = 0; r < 4; ++r)
+                            t[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+            } else {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            t[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LD + wn * WN + j * 32 + (lane & 31)] =
+                                acc[i][j][r];
+            }
         }
         __syncthreads();
         for (int c = threadIdx.x; c < WM * CPR; c += NT) {
@@ -357,12 +370,17 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(GemmArgs a) {
 // IL = 1: the next stage's DMA pieces are issued between this step's fragment reads and MFMAs (half after the
 // first K half's reads, half after the second's) instead of all of them right after the barrier, so the wave's
 // LDS reads are in flight while the pieces queue at the texture unit and the fill overlaps the MFMAs.
+// MF = 32: v_mfma_f32_32x32x16_bf16 on 32x32 fragments (tile images in swizzle family 1, tiles.h frag32), half the
+// MFMA instructions of the 16x16x32 form for the same wave tile; no in-loop bias sums, staged epilogue only.
 template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
-          int IL = 0>
+          int IL = 0, int MF = 16>
 __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid) {
+    static_assert(MF == 16 || (MF == 32 && !DIRECT && IL == 0), "32x32x16 MFMA: staged epilogue, no interleaved issue");
+    constexpr int SW = MF == 32 ? 1 : 0;
     constexpr int NW = WGM * WGN;
     constexpr int WM = BM / WGM, WN = BN / WGN;
-    constexpr int FM = WM / 16, FN = WN / 16;
+    constexpr int FM = WM / MF, FN = WN / MF;
+    static_assert(FM >= 1 && FN >= 1 && FM * MF == WM && FN * MF == WN, "wave tile must be a multiple of the MFMA tile");
     constexpr int A_BYTES = BM * GEMM_BK * 2, B_BYTES = BN * GEMM_BK * 2;
     constexpr int STAGE = A_BYTES + B_BYTES;
     constexpr int LPS = GldsTile<BM, A_KM, NW>::PER_WAVE + GldsTile<BN, B_KN, NW>::PER_WAVE;  // vmcnt per stage
@@ -385,34 +403,35 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / WGN, wn = wave % WGN;
 
-    f32x4 acc[FM][FN];
+    using AccT = std::conditional_t<MF == 32, f32x16, f32x4>;
+    AccT acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FN; ++j) acc[i][j] = AccT{};
 
     auto issue_stage = [&](int kt) {
         char* st = smem + (kt % NS) * STAGE;
         const int k0 = kbeg + kt * GEMM_BK;
-        GldsTile<BM, A_KM, NW>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
-        GldsTile<BN, B_KN, NW>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
+        GldsTile<BM, A_KM, NW, SW>::issue(st, a.A, a.lda, m0, a.M, k0, wave);
+        GldsTile<BN, B_KN, NW, SW>::issue(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave);
     };
     constexpr int PA = GldsTile<BM, A_KM, NW>::PER_WAVE;
     auto issue_piece = [&](int kt, int p) {  // piece p of this wave's LPS pieces of stage kt (A's first)
         char* st = smem + (kt % NS) * STAGE;
         const int k0 = kbeg + kt * GEMM_BK;
-        if (p < PA) GldsTile<BM, A_KM, NW>::issue_piece(st, a.A, a.lda, m0, a.M, k0, wave, p);
-        else GldsTile<BN, B_KN, NW>::issue_piece(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave, p - PA);
+        if (p < PA) GldsTile<BM, A_KM, NW, SW>::issue_piece(st, a.A, a.lda, m0, a.M, k0, wave, p);
+        else GldsTile<BN, B_KN, NW, SW>::issue_piece(st + A_BYTES, a.B, a.ldb, n0, a.N, k0, wave, p - PA);
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue_stage(s);
 
-    FragReader<BM, A_KM> la;
-    FragReader<BN, B_KN> lb;
+    FragReader<BM, A_KM, SW> la;
+    FragReader<BN, B_KN, SW> lb;
     // weight-gradient bias: the waves of the last tile row with wm == 0 also sum the B (dY) fragments they
-    // read: lane l holds B[k = 8(l>>4) .. +7][n = l & 15] of each 16-column fragment
-    constexpr bool CS = A_KM && B_KN && EPI == ERGM_EPI_NONE && !OUT_BF16;
+    // read: lane l holds B[k = 8(l>>4) .. +7][n = l & 15] of each 16-column fragment (16x16x32 form only)
+    constexpr bool CS = A_KM && B_KN && EPI == ERGM_EPI_NONE && !OUT_BF16 && MF == 16;
     const bool do_cs = CS && a.colsum && tm == a.tiles_m - 1 && wm == 0;
     float cs[FN];
 #pragma unroll
@@ -430,6 +449,21 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
             const bool refill = kt + NS - 1 < nk;
             if (!IL && refill) issue_stage(kt + NS - 1);
             const char* st = smem + (kt % NS) * STAGE;
+            if constexpr (MF == 32) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) fa[i] = la.frag32(st, wm * WM + i * 32, kk);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) fb[j] = lb.frag32(st + A_BYTES, wn * WN + j * 32, kk);
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+            } else {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 bf16x8 fa[FM], fb[FN];
@@ -466,6 +500,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
                     }
             }
+            }
         }
     };
     if constexpr (CS) {
@@ -497,7 +532,8 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
         store_tile_direct<WGN, EPI, OUT_BF16, FM, FN, WM, WN>(a, acc, m0, n0, alpha);
     } else {
         float* slab = a.slab ? a.slab + (size_t)zs * a.M * a.N : nullptr;
-        store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN>(a, smem, acc, m0, n0, alpha, slab);
+        store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * WGM * WGN, false, false, MF>(a, smem, acc, m0, n0, alpha,
+                                                                                           slab);
     }
 }
 
@@ -617,9 +653,9 @@ __global__ __launch_bounds__(128 * WGM * WGN) void gemm_ks2_kernel(GemmArgs a) {
 }
 
 template <int BM, int BN, int WGM, int WGN, int NS, bool A_KM, bool B_KN, int EPI, bool OUT_BF16, bool DIRECT = false,
-          int IL = 0>
+          int IL = 0, int MF = 16>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(GemmArgs a) {
-    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT, IL>(a, blockIdx.x);
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, A_KM, B_KN, EPI, OUT_BF16, DIRECT, IL, MF>(a, blockIdx.x);
 }
 
 // Two weight-gradient GEMMs (KM x KN, f32 out, no split) in ONE launch: workgroups [0, b1) run problem 0
@@ -631,13 +667,13 @@ struct GemmArgs2 {
     GemmArgs a[2];
     int b1;
 };
-template <int BM, int BN, int WGM, int WGN, int NS, int IL = 0, int EPI = ERGM_EPI_NONE>
+template <int BM, int BN, int WGM, int WGN, int NS, int IL = 0, int EPI = ERGM_EPI_NONE, int MF = 16>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_dw2_kernel(GemmArgs2 g) {
     const int b = blockIdx.x;
     const int pr = b < g.b1 ? 0 : 1;
     const int bb = pr == 0 ? b : b - g.b1;
     if (pr == 0 && b >= g.a[0].tiles_m * g.a[0].tiles_n) return;
-    gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, EPI, false, false, IL>(g.a[pr], bb);
+    gemm_pipe_body<BM, BN, WGM, WGN, NS, true, true, EPI, false, false, IL, MF>(g.a[pr], bb);
 }
 
 // Warp-specialised variant: NP producer waves only issue the LDS-DMA fills, the WGM x WGN consumer
@@ -966,6 +1002,7 @@ struct PipeCfg {
     bool direct = false;  // LDS-free epilogue (store_tile_direct); split-K partials keep the staged one
     int il = 0;      // 1: next-stage DMA pieces interleaved with the step's reads / MFMAs (gemm_pipe_body IL)
     int ks = 1;      // 2: intra-workgroup split-K over two wave groups (gemm_ks2_body; ns counts K-step pairs)
+    int mf = 16;     // 32: v_mfma_f32_32x32x16_bf16 on 32x32 fragments (gemm_pipe_body MF; pipelined kernel only)
 };
 static constexpr PipeCfg kCfgs[] = {
     {64, 64, 2, 2, 4},     // 0
@@ -1010,6 +1047,16 @@ static constexpr PipeCfg kCfgs[] = {
     {64, 128, 2, 2, 2, 0, false, 0, 2},   // 35  96 KB
     {128, 64, 2, 2, 2, 0, false, 0, 2},   // 36  96 KB
     {128, 128, 2, 2, 2, 0, false, 0, 2},  // 37 128 KB
+    // v_mfma_f32_32x32x16_bf16 twins of the pipelined configurations (round 6, verdict r05 #2)
+    {64, 64, 2, 2, 4, 0, false, 0, 1, 32},     // 38 cfg 0
+    {128, 128, 2, 2, 2, 0, false, 0, 1, 32},   // 39 cfg 2
+    {128, 128, 4, 2, 2, 0, false, 0, 1, 32},   // 40 cfg 10 (32 x 64 per wave)
+    {128, 64, 2, 2, 4, 0, false, 0, 1, 32},    // 41 cfg 7
+    {64, 128, 2, 2, 4, 0, false, 0, 1, 32},    // 42 cfg 8
+    {128, 128, 4, 2, 4, 0, false, 0, 1, 32},   // 43 cfg 15
+    {256, 256, 4, 2, 2, 0, false, 0, 1, 32},   // 44 cfg 6 (64 x 128 per wave)
+    {64, 64, 2, 2, 8, 0, false, 0, 1, 32},     // 45 cfg 11
+    {128, 128, 2, 4, 3, 0, false, 0, 1, 32},   // 46 cfg 3 (64 x 32 per wave)
 };
 static constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -1197,8 +1244,8 @@ static void launch_pipe_cfg(const GemmArgs& a, int split, hipStream_t s) {
         k_split = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, ERGM_EPI_NONE, false>;
         k_full = gemm_ws_kernel<c.bm, c.bn, c.wgm, c.wgn, c.np, c.ns, AKM, BKN, EPI, OB>;
     } else {
-        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false, false, c.il>;
-        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct, c.il>;
+        k_split = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, ERGM_EPI_NONE, false, false, c.il, c.mf>;
+        k_full = gemm_pipe_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, AKM, BKN, EPI, OB, c.direct, c.il, c.mf>;
     }
     static bool attr = (hipFuncSetAttribute((const void*)k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                         hipFuncSetAttribute((const void*)k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -1249,7 +1296,16 @@ static void launch_pipe(const GemmArgs& a, int cfg, int split, hipStream_t s) {
         case 34: launch_pipe_cfg<34, AKM, BKN, EPI, OB>(a, split, s); break;
         case 35: launch_pipe_cfg<35, AKM, BKN, EPI, OB>(a, split, s); break;
         case 36: launch_pipe_cfg<36, AKM, BKN, EPI, OB>(a, split, s); break;
-        default: launch_pipe_cfg<37, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 37: launch_pipe_cfg<37, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 38: launch_pipe_cfg<38, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 39: launch_pipe_cfg<39, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 40: launch_pipe_cfg<40, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 41: launch_pipe_cfg<41, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 42: launch_pipe_cfg<42, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 43: launch_pipe_cfg<43, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 44: launch_pipe_cfg<44, AKM, BKN, EPI, OB>(a, split, s); break;
+        case 45: launch_pipe_cfg<45, AKM, BKN, EPI, OB>(a, split, s); break;
+        default: launch_pipe_cfg<46, AKM, BKN, EPI, OB>(a, split, s); break;
     }
 }
 
@@ -1634,10 +1690,10 @@ static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B,
     a.nt_store = (d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
                  (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE);
     // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
-    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1;
+    const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 && kCfgs[p.cfg].mf == 16;
     a.colsum = cs_in ? d->bias_grad : nullptr;
     a.colsum_part = nullptr;
-    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 ? 1 : 0;
+    a.xcd_split = p.xcd && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 && kCfgs[p.cfg].mf == 16 ? 1 : 0;
     return a;
 }
 }  // namespace ergm
@@ -1726,7 +1782,7 @@ static void launch_dw2_cfg(const GemmArgs2& g, int nblocks, hipStream_t s) {
     constexpr PipeCfg c = kCfgs[C];
     static_assert(c.np == 0 && !c.direct, "grouped dW launch: pipelined kernels with the staged epilogue only");
     constexpr size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * GEMM_BK * 2, (size_t)(c.bm / c.wgm) * (c.bn + 4) * 4);
-    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il, EPI>;
+    auto k = gemm_dw2_kernel<c.bm, c.bn, c.wgm, c.wgn, c.ns, c.il, EPI, c.mf>;
     static bool attr = (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), true);
     (void)attr;
     ERGM_LAUNCH(k, dim3(nblocks), dim3(64 * c.wgm * c.wgn), lds, s, g);
@@ -1745,7 +1801,8 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
     }
     GemmPlan p[2] = {plan_gemm(d[0]), plan_gemm(d[1])};
     const int cfg = p[0].cfg;
-    if (cfg < 0 || (cfg >= 16 && kCfgs[cfg].il == 0) || kCfgs[cfg].ks != 1 || p[1].cfg != cfg || p[0].split != 1 ||
+    if (cfg < 0 || (cfg >= 16 && cfg < 38 && kCfgs[cfg].il == 0) || kCfgs[cfg].ks != 1 || p[1].cfg != cfg ||
+        p[0].split != 1 ||
         p[1].split != 1 ||
         p[0].xcd || p[1].xcd || kCfgs[cfg].np != 0 || kCfgs[cfg].direct)
         return ERGM_EUNSUPPORTED;
@@ -1786,6 +1843,15 @@ int gemm_dw_pair(const ergm_gemm_desc* const d[2], const void* const A[2], const
         case 30: launch_dw2_cfg<30>(g, nb, s); break;
         case 31: launch_dw2_cfg<31>(g, nb, s); break;
         case 32: launch_dw2_cfg<32>(g, nb, s); break;
+        case 38: launch_dw2_cfg<38>(g, nb, s); break;
+        case 39: launch_dw2_cfg<39>(g, nb, s); break;
+        case 40: launch_dw2_cfg<40>(g, nb, s); break;
+        case 41: launch_dw2_cfg<41>(g, nb, s); break;
+        case 42: launch_dw2_cfg<42>(g, nb, s); break;
+        case 43: launch_dw2_cfg<43>(g, nb, s); break;
+        case 44: launch_dw2_cfg<44>(g, nb, s); break;
+        case 45: launch_dw2_cfg<45>(g, nb, s); break;
+        case 46: launch_dw2_cfg<46>(g, nb, s); break;
         default: return ERGM_EUNSUPPORTED;
     }
     return check_launch("gemm_dw_pair");

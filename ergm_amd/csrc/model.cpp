@@ -174,6 +174,8 @@ struct ergm_model_plan {
     float *dh, *dy, *dcap, *delta;
     __bf16* dyb;  // the block LayerNorms' incoming gradient: their data-gradient GEMM's bf16 output (ln_f's: dy, f32)
     bool ln_dy_f32;  // ERGM_LN_DY_F32=1: the block LayerNorms read an f32 data-gradient GEMM output (dy) instead
+    bool bind_forks;  // fork points bound to the producing launch (arm_fork); ERGM_BIND_FORKS=0: recorded events only
+    bool lm_dw_first;  // ERGM_LMHEAD_DW_FIRST=1: the LM-head dW is forked before the LM-head dX GEMM (they run together)
     __bf16 *d_o, *dkv_all;
     // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
     // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
@@ -473,7 +475,7 @@ hipEvent_t stream_point(ergm_model_plan* P, hipStream_t s, hipEvent_t ev) {
 }
 // Bind the next fork point of `s` to the launches that follow on s (the stage's producer of the fork).
 void arm_fork(ergm_model_plan* P, hipStream_t s) {
-    if (!P->dry) bind_arm(s, P->ev_fork);
+    if (!P->dry && P->bind_forks) bind_arm(s, P->ev_fork);
 }
 
 // Make the side stream wait for everything issued so far on `s` (the producer of a dW GEMM's dY).
@@ -771,6 +773,10 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_FP8_MX")) P->mx = atoi(e) != 0;
     P->ln_dy_f32 = false;
     if (const char* e = getenv("ERGM_LN_DY_F32")) P->ln_dy_f32 = atoi(e) != 0;
+    P->bind_forks = true;
+    if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
+    P->lm_dw_first = false;
+    if (const char* e = getenv("ERGM_LMHEAD_DW_FIRST")) P->lm_dw_first = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
     P->dw_group = d.n_embd < 1024;
@@ -1301,20 +1307,22 @@ int do_backward_head(ergm_model_plan* P, const float* gscale, hipStream_t s) {
         lm_scale = nullptr;
     }
     P->logits_grad = nullptr;
-    {
-        Probe pr(P, 2, s);
-        ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
-                      nullptr, nullptr, 0, nullptr, 0, lm_scale));
-    }
-    {
+    auto lm_dw = [&]() -> int {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
         Probe pr(P, 3, ss);
         Probe pr5(P, 5, ss, 2.0 * Vp * E * T);
         ERGM_TRY(gemm(P, ss, Vp, E, T, P->dlogits, Vp, ERGM_KM, P->lnf, E, ERGM_KN, p.g_wte, E, ERGM_F32,
                       ERGM_EPI_NONE, nullptr, nullptr, 0, nullptr, 0, lm_scale));
-        ERGM_TRY(side_mark(P, L + 1));
+        return side_mark(P, L + 1);
+    };
+    if (P->lm_dw_first) ERGM_TRY(lm_dw());
+    {
+        Probe pr(P, 2, s);
+        ERGM_TRY(gemm(P, s, T, E, Vp, P->dlogits, Vp, ERGM_MK, p.wte_b, E, ERGM_KN, P->dy, E, ERGM_F32, ERGM_EPI_NONE,
+                      nullptr, nullptr, 0, nullptr, 0, lm_scale));
     }
+    if (!P->lm_dw_first) ERGM_TRY(lm_dw());
     if (P->dry) return ERGM_OK;
     if (P->emo_labels) {
         ERGM_TRY(ergm_emotion_head(P->lnf, p.emo_w, P->emo_labels, P->emo_tmp, P->emo_tmp + (size_t)B * 7, p.g_emo_w,

@@ -18,7 +18,19 @@ __device__ __forceinline__ int swz_row(int row) { return row & 7; }  // 128-B ro
 __device__ __forceinline__ int swz_tr16(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }        // 256-B rows
 __device__ __forceinline__ int swz_tr8(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }  // 128-B rows
 
-template <int ROWS, bool TRANS>
+// Swizzle family SW of a tile image (the DMA writes and the fragment reads of one kernel use the same one):
+//   SW 0 — the v_mfma_f32_16x16x32_bf16 reads above;
+//   SW 1 — the v_mfma_f32_32x32x16_bf16 reads (frag32): a row read (ds_read_b128, lanes 0-31 rows r0..r0+31 of one
+//   16-B chunk) is conflict-free in each of the instruction's four 16-lane groups with chunk ^ ((row >> 1) & 7); a
+//   transposed read (ds_read_b64_tr_b16, a 32-lane half takes 4 k-rows x 32 columns = 4 chunks per row) with chunk ^
+//   4·(k & 3) on rows of >= 256 B and chunk ^ 4·((k >> 1) & 1) on 128-B rows (cdna_hip_programming.md T10, §2).
+template <bool TRANS, int CPR, int SW>
+__device__ __forceinline__ int swz_of(int row) {
+    if constexpr (SW == 0) return TRANS ? (CPR == 16 ? swz_tr16(row) : swz_tr8(row)) : swz_row(row);
+    else return TRANS ? (CPR == 8 ? ((row >> 1) & 1) << 2 : (row & 3) << 2) : (row >> 1) & 7;
+}
+
+template <int ROWS, bool TRANS, int SW = 0>
 struct TileLoader {
     // ROWS = tile extent along M (A) or N (B).  !TRANS: tile [ROWS][64] (k contiguous);
     // TRANS: tile [64][ROWS] (ROWS contiguous).
@@ -56,9 +68,7 @@ struct TileLoader {
         for (int i = 0; i < PER_THREAD; ++i) {
             int c = threadIdx.x + i * GEMM_THREADS;
             int lrow = c / CPR, lc = c % CPR;
-            int pc;
-            if (!TRANS) pc = lc ^ swz_row(lrow);
-            else pc = lc ^ (CPR == 16 ? swz_tr16(lrow) : swz_tr8(lrow));
+            const int pc = lc ^ swz_of<TRANS, CPR, SW>(lrow);
             *reinterpret_cast<uint4*>(lds + lrow * ROW_BYTES + pc * 16) = regs[i];
         }
     }
@@ -69,17 +79,42 @@ struct TileLoader {
         if (!TRANS) {
             int row = ro + (lane & 15);
             int ch = ks * 4 + (lane >> 4);
-            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ swz_row(row)) << 4));
+            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ swz_of<TRANS, CPR, SW>(row)) << 4));
         } else {
             int i16 = lane & 15, g = lane >> 4;
             int k = ks * 32 + 8 * g + (i16 >> 2);
             int col = ro + 4 * (i16 & 3);
             int ch = col >> 3;
             int sub = (col & 7) * 2;  // byte offset within chunk (0 or 8)
-            int s1 = CPR == 16 ? swz_tr16(k) : swz_tr8(k);
-            int s2 = CPR == 16 ? swz_tr16(k + 4) : swz_tr8(k + 4);
+            int s1 = swz_of<TRANS, CPR, SW>(k);
+            int s2 = swz_of<TRANS, CPR, SW>(k + 4);
             const char* p1 = lds + k * ROW_BYTES + ((ch ^ s1) << 4) + sub;
             const char* p2 = lds + (k + 4) * ROW_BYTES + ((ch ^ s2) << 4) + sub;
+            s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p1));
+            s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p2));
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            return __builtin_bit_cast(bf16x8, r);
+        }
+    }
+    // MFMA 32x32x16 operand fragment for the 32 rows starting at `ro`, 16-deep k-step kk (0..3) of the 64-deep stage.
+    // Lane l gets element j = X[ro + (l&31)][16kk + 8(l>>5) + j] (the v_mfma_f32_32x32x16_bf16 A / B lane map).
+    __device__ __forceinline__ bf16x8 frag32(const char* lds, int ro, int kk) const {
+        const int lane = threadIdx.x & 63;
+        if (!TRANS) {
+            const int row = ro + (lane & 31);
+            const int ch = kk * 2 + (lane >> 5);
+            return *reinterpret_cast<const bf16x8*>(lds + row * ROW_BYTES + ((ch ^ swz_of<TRANS, CPR, SW>(row)) << 4));
+        } else {
+            // per 16-lane group G: rows k0..k0+3 (then +4..+7) of the 16 columns ro + 16(G&1) ...; lane 4q+p addresses
+            // row q, columns 4p..4p+3, and receives its column's 4 rows (T10)
+            const int i16 = lane & 15, G = lane >> 4;
+            const int k = kk * 16 + 8 * (G >> 1) + (i16 >> 2);
+            const int col = ro + 16 * (G & 1) + 4 * (i16 & 3);
+            const int ch = col >> 3;
+            const int sub = (col & 7) * 2;
+            const char* p1 = lds + k * ROW_BYTES + ((ch ^ swz_of<TRANS, CPR, SW>(k)) << 4) + sub;
+            const char* p2 = lds + (k + 4) * ROW_BYTES + ((ch ^ swz_of<TRANS, CPR, SW>(k + 4)) << 4) + sub;
             s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p1));
             s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p2));
             typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -141,7 +176,7 @@ __device__ __forceinline__ uint32_t lds_addr_of(const char* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int ROWS, bool TRANS, int NWAVES>
+template <int ROWS, bool TRANS, int NWAVES, int SW = 0>
 struct GldsTile {
     static constexpr int BYTES = ROWS * GEMM_BK * 2;
     static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;   // wave-instructions per wave per stage
@@ -159,11 +194,11 @@ struct GldsTile {
         const int row = o / ROW_BYTES, pc = (o % ROW_BYTES) >> 4;
         const __bf16* src;
         if (!TRANS) {
-            const int c = pc ^ swz_row(row);
+            const int c = pc ^ swz_of<TRANS, CPR, SW>(row);
             const int r = min(r0 + row, Rlim - 1);
             src = base + (size_t)r * ld + k0 + c * 8;
         } else {
-            const int c = pc ^ (CPR == 16 ? swz_tr16(row) : swz_tr8(row));
+            const int c = pc ^ swz_of<TRANS, CPR, SW>(row);
             const int col = min(r0 + c * 8, ((Rlim + 7) & ~7) - 8);
             src = base + (size_t)(k0 + row) * ld + col;
         }
@@ -177,7 +212,7 @@ struct GldsTile {
 };
 
 // Fragment reader for a staged tile (any wave count): same LDS image and swizzles as TileLoader.
-template <int ROWS, bool TRANS>
-using FragReader = TileLoader<ROWS, TRANS>;
+template <int ROWS, bool TRANS, int SW = 0>
+using FragReader = TileLoader<ROWS, TRANS, SW>;
 
 }  // namespace ergm

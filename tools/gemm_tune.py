@@ -52,7 +52,9 @@ CFGS = [(64, 64), (128, 128), (128, 128), (128, 128), (256, 128), (128, 256), (2
         (64, 64), (64, 64), (128, 64), (64, 128), (128, 128), (128, 128),
         (256, 256), (128, 128), (128, 128),                       # 22-24 LDS-free epilogue variants
         (64, 64), (128, 128), (128, 128), (256, 256), (64, 128), (128, 128), (128, 128), (128, 128),  # 25-32 IL
-        (64, 64), (64, 64), (64, 128), (128, 64), (128, 128)]                                         # 33-37 KS2
+        (64, 64), (64, 64), (64, 128), (128, 64), (128, 128),                                         # 33-37 KS2
+        (64, 64), (128, 128), (128, 128), (128, 64), (64, 128), (128, 128), (256, 256), (64, 64), (128, 128)]  # 38-46
+# 38-46: the v_mfma_f32_32x32x16_bf16 twins of cfgs 0, 2, 10, 7, 8, 15, 6, 11, 3
 REPS = 20
 
 
@@ -165,7 +167,7 @@ def main():
             bm, bn = CFGS[cfg]
             tiles = -(-M // bm) * -(-N // bn)
             splits = [1]
-            if tiles < 400:
+            if tiles < 400 and "--nosplit" not in sys.argv:
                 splits += [s for s in (2, 3, 4, 6, 8) if K // s >= 256 and tiles * s <= 2048]
             for sp in splits:
                 try:

@@ -27,14 +27,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from ergm_amd import _lib as L  # noqa: E402
 
-CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13, 22, 23, 24]  # kCfgs indices (gemm.hip)
+CANDIDATES = [0, 2, 10, 14, 15, 6, 4, 9, 1, 3, 7, 8, 11, 12, 13, 22, 23, 24,
+              38, 39, 40, 41, 42, 43, 44, 45, 46]  # kCfgs indices (gemm.hip); 38-46: v_mfma_f32_32x32x16_bf16
 F8_TILE = {0: (128, 128), 1: (256, 128), 2: (128, 128), 3: (256, 256), 4: (64, 64)}  # kF8Cfgs (gemm.hip)
 TILE = {0: (64, 64), 1: (128, 128), 2: (128, 128), 3: (128, 128), 4: (256, 128), 6: (256, 256), 7: (128, 64),
         8: (64, 128), 9: (256, 128), 10: (128, 128), 11: (64, 64), 12: (128, 64), 13: (64, 128), 14: (128, 128),
         15: (128, 128), 16: (64, 64), 17: (64, 64), 18: (128, 64), 19: (64, 128), 20: (128, 128), 21: (128, 128),
         22: (256, 256), 23: (128, 128), 24: (128, 128), 25: (64, 64), 26: (128, 128), 27: (128, 128),
         28: (256, 256), 29: (64, 128), 30: (128, 128), 31: (128, 128), 32: (128, 128), 33: (64, 64), 34: (64, 64),
-        35: (64, 128), 36: (128, 64), 37: (128, 128)}
+        35: (64, 128), 36: (128, 64), 37: (128, 128), 38: (64, 64), 39: (128, 128), 40: (128, 128), 41: (128, 64),
+        42: (64, 128), 43: (128, 128), 44: (256, 256), 45: (64, 64), 46: (128, 128)}
 
 
 def main():
