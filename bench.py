@@ -284,7 +284,7 @@ def main():
     kw = {k: v.to(dev) for k, v in kw.items()}  # inputs resident in HBM before timing
     aud_hidden = None
     if big_feat:  # wav2vec2-shaped encoder output, pooled inside every timed step
-        from ergm_amd.features import mean_pool
+        from ergm_amd.ops import feat_pool
         aud_hidden = (0.1 * torch.randn(B, 400, Fd, generator=torch.Generator().manual_seed(7 + rank))).to(dev)
     loss_acc = torch.zeros(2, device=dev)
     correct = torch.zeros(1, device=dev, dtype=torch.int64)
@@ -295,7 +295,7 @@ def main():
 
     def step():
         if aud_hidden is not None:
-            kw["auds"] = mean_pool(aud_hidden)
+            kw["auds"] = feat_pool(aud_hidden)
         out = model(**kw)
         opt.zero_grad()
         out.loss.backward()

@@ -84,12 +84,15 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int m, int n, 
 }
 
 // Vectorized epilogue for 8 consecutive columns n..n+7 of row m (N % 8 == 0, n % 8 == 0).
+// pre_bias / pre_aux: the bias (2 float4) and aux operand (BIAS_RESID: 2 float4 of the residual; GELU_BWD: one float4
+// holding 8 bf16) of these 8 columns, loaded before the main loop (EpiPre) — nullptr: loaded here.
 template <int EPI, bool OUT_BF16>
-__device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n, float* v) {
+__device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n, float* v,
+                                                const float4* pre_bias = nullptr, const float4* pre_aux = nullptr) {
     if (EPI == ERGM_EPI_BIAS || EPI == ERGM_EPI_BIAS_GELU || EPI == ERGM_EPI_BIAS_RESID) {
         if (a.bias) {
-            float4 b0 = *reinterpret_cast<const float4*>(a.bias + n);
-            float4 b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
+            float4 b0 = pre_bias ? pre_bias[0] : *reinterpret_cast<const float4*>(a.bias + n);
+            float4 b1 = pre_bias ? pre_bias[1] : *reinterpret_cast<const float4*>(a.bias + n + 4);
             v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
             v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
@@ -110,11 +113,13 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
             for (int j = 0; j < 8; ++j) v[j] = ((k >> j) & 1u) ? v[j] * a.drop.scale : 0.f;
         }
         const float* r = reinterpret_cast<const float*>(a.aux) + (size_t)m * a.ld_aux + n;
-        float4 r0 = *reinterpret_cast<const float4*>(r), r1 = *reinterpret_cast<const float4*>(r + 4);
+        float4 r0 = pre_aux ? pre_aux[0] : *reinterpret_cast<const float4*>(r);
+        float4 r1 = pre_aux ? pre_aux[1] : *reinterpret_cast<const float4*>(r + 4);
         v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
     } else if (EPI == ERGM_EPI_GELU_BWD) {  // v · gelu_new'(pre), the derivative stored by the forward
-        bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.aux) + (size_t)m * a.ld_aux + n);
+        bf16x8 x = pre_aux ? __builtin_bit_cast(bf16x8, pre_aux[0])
+                           : *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.aux) + (size_t)m * a.ld_aux + n);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= bf2f(x[j]);
     }
@@ -147,6 +152,45 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
     }
 }
 
+// Epilogue operands loaded before the main loop: a BIAS_RESID / GELU_BWD epilogue reads the residual (f32) / the
+// stored gelu' (bf16) of its tile and the bias, and at the end of the kernel those loads' latency is exposed (every
+// wave waits for them with nothing left to overlap).  When store_tile gives each thread exactly one 8-column chunk per
+// pass (WM·CPR == NT), the thread knows its chunks up front and loads them while the K loop runs: WGM·8 floats (or
+// WGM·8 bf16) + 8 bias floats of registers.  Same values, same arithmetic: the output is bitwise unchanged.
+template <int EPI, int BM, int BN, int WGM, int NT>
+struct EpiPre {
+    static constexpr int WM = BM / WGM, CPR = BN / 8;
+    static constexpr int PER = EPI == ERGM_EPI_BIAS_RESID ? 2 : 1;  // float4 per chunk
+    static constexpr bool ON = (EPI == ERGM_EPI_BIAS_RESID || EPI == ERGM_EPI_GELU_BWD) && WM * CPR == NT &&
+                               WGM * PER <= 4;
+    float4 aux[ON ? WGM * PER : 1];
+    float4 bias[2];
+    __device__ __forceinline__ void load(const GemmArgs& a, int m0, int n0) {
+        if constexpr (ON) {
+            if (a.slab) return;  // split-K partials: the reduce kernel applies the epilogue
+            const int row = threadIdx.x / CPR, n = n0 + (threadIdx.x % CPR) * 8;
+            if (n >= a.N) return;
+            if (EPI == ERGM_EPI_BIAS_RESID && a.bias) {
+                bias[0] = *reinterpret_cast<const float4*>(a.bias + n);
+                bias[1] = *reinterpret_cast<const float4*>(a.bias + n + 4);
+            }
+#pragma unroll
+            for (int p = 0; p < WGM; ++p) {
+                const int m = m0 + p * WM + row;
+                if (m >= a.M) continue;
+                if constexpr (EPI == ERGM_EPI_BIAS_RESID) {
+                    const float* r = reinterpret_cast<const float*>(a.aux) + (size_t)m * a.ld_aux + n;
+                    aux[2 * p] = *reinterpret_cast<const float4*>(r);
+                    aux[2 * p + 1] = *reinterpret_cast<const float4*>(r + 4);
+                } else {
+                    aux[p] = *reinterpret_cast<const float4*>(reinterpret_cast<const __bf16*>(a.aux) +
+                                                              (size_t)m * a.ld_aux + n);
+                }
+            }
+        }
+    }
+};
+
 // Write a BM x BN accumulator tile (WGM x WGN waves, 16x16 MFMA fragments) through LDS so that every
 // global store is a coalesced 16-B (bf16) / 32-B (f32) row piece instead of per-lane 2/4-B scatters
 // (the per-lane form made the large GEMMs store-issue bound).  One wave-row (BM/WGM rows) per pass, so
@@ -156,7 +200,7 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& a, int m, int n,
 template <int BM, int BN, int WGM, int WGN, int EPI, bool OUT_BF16, int FM, int FN, int NT = 64 * WGM * WGN,
           bool RS = false, bool QMX = false, int MF = 16, typename AccT = f32x4>
 __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, AccT (&acc)[FM][FN], int m0, int n0,
-                                           float alpha, float* slab) {
+                                           float alpha, float* slab, const EpiPre<EPI, BM, BN, WGM, NT>* pre = nullptr) {
     // NT: every thread of the workgroup (a warp-specialised kernel adds producer waves, which only
     // help with the copy-out; accumulator fragments come from the WGM x WGN consumer waves)
     constexpr int LD = BN + 4;  // lanes l and l+16 (rows 4 apart) land 16 banks apart
@@ -229,6 +273,13 @@ __device__ __forceinline__ void store_tile(const GemmArgs& a, char* lds, AccT (&
                     const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
                     for (int j = 0; j < 8; ++j) v[j] *= sa * sb[j];
+                }
+                if constexpr (EpiPre<EPI, BM, BN, WGM, NT>::ON) {
+                    if (pre) {  // c == threadIdx.x: this thread's chunk of pass `pass`, loaded before the K loop
+                        constexpr int PER = EpiPre<EPI, BM, BN, WGM, NT>::PER;
+                        epilogue_store8<EPI, OUT_BF16>(a, m, n, v, pre->bias, pre->aux + PER * pass);
+                        continue;
+                    }
                 }
                 epilogue_store8<EPI, OUT_BF16>(a, m, n, v);
             }
@@ -427,6 +478,8 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue_stage(s);
 
+    EpiPre<EPI, BM, BN, WGM, 64 * NW> pre;
+    if constexpr (!DIRECT) pre.load(a, m0, n0);
     FragReader<BM, A_KM, SW> la;
     FragReader<BN, B_KN, SW> lb;
     // weight-gradient bias: the waves of the last tile row with wm == 0 also sum the B (dY) fragments they
@@ -533,7 +586,7 @@ __device__ __forceinline__ void gemm_pipe_body(const GemmArgs& a, const int bid)
     } else {
         float* slab = a.slab ? a.slab + (size_t)zs * a.M * a.N : nullptr;
         store_tile<BM, BN, WGM, WGN, EPI, OUT_BF16, FM, FN, 64 * WGM * WGN, false, false, MF>(a, smem, acc, m0, n0, alpha,
-                                                                                           slab);
+                                                                                           slab, &pre);
     }
 }
 

@@ -143,6 +143,10 @@ struct ergm_model_plan {
     uint8_t *capkv8_x, *xa, *xf, *xcap;
     unsigned* capkv_amax;
     std::vector<hipEvent_t> ev_wq;
+    // the caption K/V projection of block l done on the side stream (kv_per_block): block l's cross-attention waits
+    // for ev_kv[l] only, so the later blocks' projections overlap the latency-bound forward
+    std::vector<hipEvent_t> ev_kv;
+    bool kv_per_block;  // one caption K/V GEMM per block (ERGM_KV_PER_BLOCK=0: one GEMM for all blocks)
     // per_stage_join: the caller's stream waits for block l+1's side-stream weight gradients at the end
     // of stage l (ergm_model_backward_layer's ordering guarantee); 0 = only the embedding stage joins,
     // consumers of a block's gradients wait with ergm_model_stage_wait instead
@@ -175,7 +179,8 @@ struct ergm_model_plan {
     __bf16* dyb;  // the block LayerNorms' incoming gradient: their data-gradient GEMM's bf16 output (ln_f's: dy, f32)
     bool ln_dy_f32;  // ERGM_LN_DY_F32=1: the block LayerNorms read an f32 data-gradient GEMM output (dy) instead
     bool bind_forks;  // fork points bound to the producing launch (arm_fork); ERGM_BIND_FORKS=0: recorded events only
-    bool lm_dw_first;  // ERGM_LMHEAD_DW_FIRST=1: the LM-head dW is forked before the LM-head dX GEMM (they run together)
+    bool lm_dw_first;  // the LM-head dW is forked before the LM-head dX GEMM, so the two run together (+0.5 % per step
+                       // at C2 over six interleaved pairs, profiles/r06_ab{2,3}.txt); ERGM_LMHEAD_DW_FIRST=0: after it
     __bf16 *d_o, *dkv_all;
     // dY operands of the weight-gradient GEMMs get one buffer per use (no reuse), so the dW GEMMs can
     // run on the side stream while the data-gradient chain continues: dhb[i] = bf16 grad of resid[i].
@@ -435,7 +440,7 @@ int gemm(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const void* A, 
 int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* ax,
           const uint8_t* Bt, const float* sb, const uint8_t* bx, void* C, int ldc, int cdt, int epi, const float* bias,
           const void* aux = nullptr, int ld_aux = 0, void* aux_out = nullptr, int ld_aux_out = 0,
-          const ergm_dropout* dropout = nullptr, uint8_t* qo = nullptr, uint8_t* qox = nullptr) {
+          const ergm_dropout* dropout = nullptr, uint8_t* qo = nullptr, uint8_t* qox = nullptr, int b_pitch = 0) {
     if (P->dry) return ERGM_OK;
     ergm_gemm_desc g;
     memset(&g, 0, sizeof(g));
@@ -444,8 +449,8 @@ int gemm8(ergm_model_plan* P, hipStream_t s, int M, int N, int K, const uint8_t*
     g.bias = bias; g.aux = aux; g.ld_aux = ld_aux; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
     g.dropout = dropout;
     // MX scale pitches (mx_sidx): activation rows (A, the MX copy of C) are token rows of a T-row buffer, B is a
-    // weight copy with exactly N rows
-    if (P->mx) return ergm_gemm_mx(&g, A, ax, P->T, Bt, bx, N, C, qo, qox, N, P->T, s);
+    // weight copy with exactly N rows (b_pitch: rows of a larger copy B is a row slice of)
+    if (P->mx) return ergm_gemm_mx(&g, A, ax, P->T, Bt, bx, b_pitch ? b_pitch : N, C, qo, qox, N, P->T, s);
     return ergm_gemm_f8(&g, A, sa, Bt, sb, C, s);
 }
 // Row quantisation of an fp8 GEMM's activation operand (attention outputs, caption embeddings; the GELU output
@@ -775,7 +780,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     if (const char* e = getenv("ERGM_LN_DY_F32")) P->ln_dy_f32 = atoi(e) != 0;
     P->bind_forks = true;
     if (const char* e = getenv("ERGM_BIND_FORKS")) P->bind_forks = atoi(e) != 0;
-    P->lm_dw_first = false;
+    P->lm_dw_first = true;
     if (const char* e = getenv("ERGM_LMHEAD_DW_FIRST")) P->lm_dw_first = atoi(e) != 0;
     // grouped pairs measured -0.2 % (C2) / -0.5 % (C4) per step at E = 768 but +0.9 % at C5 (E = 1024, whose
     // qualifying pairs are the 1025 x {1024, 3072} shapes on 128x128 tiles): on below E = 1024
@@ -796,6 +801,10 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     for (auto& e : P->ev_f2) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     P->ev_wq.assign(P->f8 ? d.n_layer : 0, nullptr);
     for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
+    P->kv_per_block = true;
+    if (const char* e = getenv("ERGM_KV_PER_BLOCK")) P->kv_per_block = atoi(e) != 0;
+    P->ev_kv.assign(P->kv_per_block ? d.n_layer : 0, nullptr);
+    for (auto& e : P->ev_kv) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
         ergm_model_destroy(P);
         return fail(ERGM_EHIP, "model_create: stream/event creation failed");
@@ -850,6 +859,8 @@ extern "C" int ergm_model_destroy(ergm_model_plan* P) {
     for (auto e : P->ev_join)
         if (e) hipEventDestroy(e);
     for (auto e : P->ev_wq)
+        if (e) hipEventDestroy(e);
+    for (auto e : P->ev_kv)
         if (e) hipEventDestroy(e);
     for (auto e : P->ev_f2)
         if (e) hipEventDestroy(e);
@@ -1057,7 +1068,13 @@ int fwd_block(ergm_model_plan* P, int l, hipStream_t s, int b0, int nb, int part
                           ERGM_EPI_BIAS, LF(P, l, ERGM_T_XQ_B)));
     }
     const __bf16* kl = P->dry ? nullptr : P->kv_all + r0 * L2E + (size_t)l * 2 * E;
-    if (on(6) && l == 0) ERGM_TRY(join_side(P, s, L));  // the caption K/V of every block (side stream)
+    if (on(6) && !P->dry) {  // the caption K/V of this block (kv_per_block) or of every block (side stream)
+        if (P->kv_per_block) {
+            if (hipStreamWaitEvent(s, P->ev_kv[l], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
+        } else if (l == 0) {
+            ERGM_TRY(join_side(P, s, L));
+        }
+    }
     if (on(6) && !P->dry) {
         if (P->xq_fuse)  // q = LN_x·Wq + bq formed inside the cross-attention forward
             ERGM_TRY(attn_fwd_qgemm(a.lnx, P->XE, LB(P, l, ERGM_T_XQ_W), E, LF(P, l, ERGM_T_XQ_B), E, a.xq, E, kl,
@@ -1168,17 +1185,18 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
         }
     }
     ERGM_TRY(embed(0));
-    // all L cross-attention K/V projections of the caption embeddings in one GEMM, on the side stream
-    // (it overlaps block 0's self-attention; joined before block 0's cross-attention)
+    // The cross-attention K/V projections of the caption embeddings, on the side stream (they overlap the chains'
+    // first sub-blocks).  kv_per_block: one GEMM per block, in block order, each marked (ev_kv[l]) for that block's
+    // cross-attention — block 0 waits for 1/L of the projection instead of all of it (the single 2048 x 18432 x 768
+    // GEMM ran alone for ~80 us at C2 while both chains waited, profiles/r06a_timeline.txt) and the rest overlaps the
+    // latency-bound forward's idle CUs (+1.7 % per step at C2, profiles/r06_ab_kv.txt).  Otherwise one GEMM for all
+    // blocks, joined (side_mark(L)) before block 0's cross-attention.
     {
         ERGM_TRY(fork_side(P, s));
         hipStream_t ss = P->dry ? s : P->side;
         for (int c = 1; c < nchain && !P->dry; ++c)  // the caption rows of every chain are embedded
             if (hipStreamWaitEvent(ss, ev_emb[c], 0) != hipSuccess) return fail(ERGM_EHIP, "model: stream wait");
         if (P->f8) ERGM_TRY(quant_layer_weights(P, 0, ss));
-        // the embedding backward's sort needs only the ids: done here, off the critical chain
-        if (train && !P->dry)
-            ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
         if (P->f8 && !P->dry) {
             if (P->mx) {
                 MxJobs J{};
@@ -1195,7 +1213,30 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
             }
             ERGM_TRY(quant_act(P, P->cap, P->XE, T, E, P->qcap, P->scap, P->xcap, ss));
         }
-        {
+        // fp8: block l's weights are re-quantised on this stream too (its forward waits for ev_wq[l]); a deferred
+        // AdamW update of block l (FusedAdamW(defer=True)) writes the bf16 shadow the quantiser reads, so the side
+        // stream waits for it like block l's forward does
+        auto quant_block = [&](int l) -> int {
+            if (!P->f8 || l <= 0 || l >= L) return ERGM_OK;
+            ERGM_TRY(wait_update(P, l, ss));
+            return quant_layer_weights(P, l, ss);
+        };
+        if (P->kv_per_block && !P->dry) {
+            for (int l = 0; l < L; ++l) {
+                const size_t c0 = (size_t)l * 2 * E;
+                if (P->f8)  // rows c0.. of the [L2E][E] weight copy and of its scales (MX pitch: all L2E rows)
+                    ERGM_TRY(gemm8(P, ss, T, 2 * E, E, P->qcap, P->scap, P->xcap, P->capkv8 + c0 * E,
+                                   P->capkv8_s ? P->capkv8_s + c0 : nullptr, P->capkv8_x ? P->capkv8_x + c0 * 4 : nullptr,
+                                   P->kv_all + c0, L2E, ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0, nullptr, 0, nullptr, 0,
+                                   nullptr, nullptr, nullptr, L2E));
+                else
+                    ERGM_TRY(gemm(P, ss, T, 2 * E, E, P->cap, P->XE, ERGM_MK,
+                                  reinterpret_cast<const __bf16*>(p.capkv_w_b) + c0, L2E, ERGM_KN, P->kv_all + c0, L2E,
+                                  ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0));
+                if (hipEventRecord(P->ev_kv[l], ss) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+                ERGM_TRY(quant_block(l + 1));  // block l+1's weights before block l+1's K/V (its forward needs both)
+            }
+        } else {
             Probe pr(P, 4, ss);
             if (P->f8)
                 ERGM_TRY(gemm8(P, ss, T, L2E, E, P->qcap, P->scap, P->xcap, P->capkv8, P->capkv8_s, P->capkv8_x,
@@ -1204,14 +1245,12 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                 ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E,
                               ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b));
         }
+        // the embedding backward's sort needs only the ids: done here, off the critical chain
+        if (train && !P->dry)
+            ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
         ERGM_TRY(side_mark(P, L));
-        if (P->f8)
-            for (int l = 1; l < L; ++l) {
-                // a deferred AdamW update of block l (FusedAdamW(defer=True)) writes the bf16 shadow the
-                // quantiser reads: the side stream waits for it like block l's forward does
-                ERGM_TRY(wait_update(P, l, ss));
-                ERGM_TRY(quant_layer_weights(P, l, ss));
-            }
+        if (!P->kv_per_block || P->dry)
+            for (int l = 1; l < L; ++l) ERGM_TRY(quant_block(l));
     }
     // Enqueue order: launch by launch, alternating chains.  The forward's kernels are short, so the host's enqueue
     // pace can set the GPU's: enqueued a block at a time, the chains ran one block after the other instead of side

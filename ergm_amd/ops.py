@@ -295,7 +295,14 @@ def embed_fwd(ids, tt, cap_ids, wte, wpe, vis=None, aud=None, dropout: Optional[
 
 def feat_pool(x: torch.Tensor, lengths: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
     """Mean over frames of encoder outputs x [B, T, D] (f32 / bf16, any row strides with unit
-    last-dim stride) -> [B, D] f32; ``lengths`` [B] int32 limits each sample to its valid frames."""
+    last-dim stride) -> [B, D] f32; ``lengths`` [B] int32 limits each sample to its valid frames.
+
+    The reference featurises offline (data_process/feature_extraction.py): wav2vec2-base-960h and BLIP-vision
+    ``last_hidden_state`` outputs ([1, T_audio, 768] / [1, 197, 768]) mean-pooled over frames / patches
+    (``torch.mean(features, dim=1)``, :63 and :69) into the 768-d vectors the model adds at positions 0 and 1
+    (src/model.py:495-498).  The encoders download from the network and are out of scope; this pools encoder
+    outputs already in HBM for a whole batch in one HIP kernel (``ergm_feat_pool``), padded audio included, so they
+    feed the model (and at config 5 its projection GEMMs) without a host round trip."""
     _need_gpu(x)
     if x.dim() != 3 or x.stride(2) != 1:
         raise ValueError("feat_pool expects [B, T, D] with contiguous feature rows")

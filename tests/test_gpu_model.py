@@ -689,6 +689,9 @@ def test_custom_op_registration_and_torch_compile(gpu):
     for compiled in (False, True):
         _, _, _, model, batch = _setup(rec, gpu)
         kw = {k: v.to(gpu) for k, v in batch.items()}
+        # a fresh Dynamo cache: a new model object can land at a freed one's address and pass its identity guard,
+        # reusing a graph traced under the other test's compiled_logits_grad (the flag is read at trace time)
+        torch._dynamo.reset()
         fn = torch.compile(model) if compiled else model
         model.flat.grad = None
         out = fn(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],
@@ -713,6 +716,9 @@ def test_compiled_logits_gradient_opt_in(gpu):
         _, _, _, model, batch = _setup(rec, gpu)
         model.compiled_logits_grad = True
         kw = {k: v.to(gpu) for k, v in batch.items()}
+        # a fresh Dynamo cache: a new model object can land at a freed one's address and pass its identity guard,
+        # reusing a graph traced under the other test's compiled_logits_grad (the flag is read at trace time)
+        torch._dynamo.reset()
         fn = torch.compile(model) if compiled else model
         model.flat.grad = None
         out = fn(input_ids=kw["input_ids"], token_type_ids=kw["token_type_ids"], labels=kw["labels"],

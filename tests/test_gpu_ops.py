@@ -472,15 +472,14 @@ def test_adamw_rows_partition_equals_full_update(gpu):
 def test_feature_mean_pooling(gpu, dtype):
     """ergm_feat_pool == torch.mean(last_hidden_state, dim=1) (data_process/feature_extraction.py:63,69),
     with per-sample valid lengths for padded audio, and on a strided (non-contiguous batch) view."""
-    from ergm_amd.features import mean_pool, pool_encoder_outputs
     g = torch.Generator().manual_seed(5)
     img = torch.randn(4, 197, 768, generator=g).to(dtype)
     aud = torch.randn(4, 401, 768, generator=g).to(dtype)
     lens = torch.tensor([401, 250, 1, 399], dtype=torch.int32)
-    v, a = pool_encoder_outputs(img.to(gpu), aud.to(gpu), lens)
+    v, a = ops.feat_pool(img.to(gpu)), ops.feat_pool(aud.to(gpu), lens)
     assert torch.allclose(v.cpu(), img.float().mean(1), rtol=1e-5, atol=1e-6)
     ref = torch.stack([aud[b, :int(lens[b])].float().mean(0) for b in range(4)])
     assert torch.allclose(a.cpu(), ref, rtol=1e-5, atol=1e-6)
     big = torch.randn(3, 50, 1024, generator=g).to(gpu)
     view = big[:, 10:40]  # batch stride 50*1024, frame stride 1024
-    assert torch.allclose(mean_pool(view).cpu(), view.float().mean(1).cpu(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(ops.feat_pool(view).cpu(), view.float().mean(1).cpu(), rtol=1e-5, atol=1e-6)

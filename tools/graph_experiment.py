@@ -1,6 +1,8 @@
 """How much would HIP-graph capture of the whole training step save?  Times the C2 step eagerly and as a
 replayed graph of one captured step (LR frozen at capture time: a timing experiment, not a training
-mode).  Usage (GPU box): python tools/graph_experiment.py"""
+mode).  Usage (GPU box): python tools/graph_experiment.py [step|fwdbwd|fwd]  (what is captured: the whole step,
+forward + backward without the optimizer, the training forward alone)"""
+import faulthandler
 import os
 import sys
 import time
@@ -11,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    faulthandler.enable()
     from ergm_amd.config import gpt2_small
     from ergm_amd.data import synthetic_batch
     from ergm_amd.model import GPT2LMHeadModel
@@ -19,7 +22,8 @@ def main():
     torch.cuda.set_device(dev)
     model = GPT2LMHeadModel(gpt2_small(), device=dev)
     model.init_weights(seed=0)
-    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=True)
+    mode = sys.argv[1] if len(sys.argv) > 1 else "step"
+    opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=mode == "step")  # no updates inside fwdbwd
     b = synthetic_batch(16, 128, n_turns=5, seed=1)
     kw = dict(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], labels=b["labels"],
               emotion_labels=b["emotion_labels"], caption_ids=b["caption_ids"], imgs=b["visual_feat"],
@@ -28,9 +32,12 @@ def main():
 
     def step():
         out = model(**kw)
+        if mode == "fwd":
+            return out
         opt.zero_grad()
         out.loss.backward()
-        opt.step()
+        if mode == "step":
+            opt.step()
         return out
 
     s = torch.cuda.Stream(dev)
@@ -44,9 +51,11 @@ def main():
         step()
     torch.cuda.synchronize()
     eager = (time.perf_counter() - t0) / K * 1e3
+    print(f"{mode}: eager {eager:.3f} ms/step; capturing", flush=True)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         step()
+    print("captured", flush=True)
     torch.cuda.synchronize()
     for _ in range(3):
         g.replay()
