@@ -1213,30 +1213,44 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
             }
             ERGM_TRY(quant_act(P, P->cap, P->XE, T, E, P->qcap, P->scap, P->xcap, ss));
         }
-        // fp8: block l's weights are re-quantised on this stream too (its forward waits for ev_wq[l]); a deferred
-        // AdamW update of block l (FusedAdamW(defer=True)) writes the bf16 shadow the quantiser reads, so the side
-        // stream waits for it like block l's forward does
-        auto quant_block = [&](int l) -> int {
-            if (!P->f8 || l <= 0 || l >= L) return ERGM_OK;
-            ERGM_TRY(wait_update(P, l, ss));
-            return quant_layer_weights(P, l, ss);
-        };
-        if (P->kv_per_block && !P->dry) {
-            for (int l = 0; l < L; ++l) {
-                const size_t c0 = (size_t)l * 2 * E;
-                if (P->f8)  // rows c0.. of the [L2E][E] weight copy and of its scales (MX pitch: all L2E rows)
-                    ERGM_TRY(gemm8(P, ss, T, 2 * E, E, P->qcap, P->scap, P->xcap, P->capkv8 + c0 * E,
-                                   P->capkv8_s ? P->capkv8_s + c0 : nullptr, P->capkv8_x ? P->capkv8_x + c0 * 4 : nullptr,
-                                   P->kv_all + c0, L2E, ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0, nullptr, 0, nullptr, 0,
-                                   nullptr, nullptr, nullptr, L2E));
-                else
-                    ERGM_TRY(gemm(P, ss, T, 2 * E, E, P->cap, P->XE, ERGM_MK,
-                                  reinterpret_cast<const __bf16*>(p.capkv_w_b) + c0, L2E, ERGM_KN, P->kv_all + c0, L2E,
-                                  ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0));
-                if (hipEventRecord(P->ev_kv[l], ss) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
-                ERGM_TRY(quant_block(l + 1));  // block l+1's weights before block l+1's K/V (its forward needs both)
-            }
-        } else {
+    }
+    hipStream_t ss = P->dry ? s : P->side;
+    // fp8: block l's weights are re-quantised on the side stream too (its forward waits for ev_wq[l]); a deferred
+    // AdamW update of block l (FusedAdamW(defer=True)) writes the bf16 shadow the quantiser reads, so the side
+    // stream waits for it like block l's forward does
+    auto quant_block = [&](int l) -> int {
+        if (!P->f8 || l <= 0 || l >= L) return ERGM_OK;
+        ERGM_TRY(wait_update(P, l, ss));
+        return quant_layer_weights(P, l, ss);
+    };
+    // the side stream's tail of forward work: the embedding backward's sort (it needs only the ids: done here, off
+    // the critical chain), then the mark
+    auto side_tail = [&]() -> int {
+        if (train && !P->dry)
+            ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
+        return side_mark(P, L);
+    };
+    const bool kvb = P->kv_per_block && !P->dry;
+    // block l's caption K/V (+ block l+1's fp8 weights); enqueued one block ahead of its cross-attention, between the
+    // chains' launches, so the host reaches the chains' first kernels without enqueuing all L projections first
+    auto kv_block = [&](int l) -> int {
+        const size_t c0 = (size_t)l * 2 * E;
+        if (P->f8)  // rows c0.. of the [L2E][E] weight copy and of its scales (MX pitch: all L2E rows)
+            ERGM_TRY(gemm8(P, ss, T, 2 * E, E, P->qcap, P->scap, P->xcap, P->capkv8 + c0 * E,
+                           P->capkv8_s ? P->capkv8_s + c0 : nullptr, P->capkv8_x ? P->capkv8_x + c0 * 4 : nullptr,
+                           P->kv_all + c0, L2E, ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0, nullptr, 0, nullptr, 0,
+                           nullptr, nullptr, nullptr, L2E));
+        else
+            ERGM_TRY(gemm(P, ss, T, 2 * E, E, P->cap, P->XE, ERGM_MK, reinterpret_cast<const __bf16*>(p.capkv_w_b) + c0,
+                          L2E, ERGM_KN, P->kv_all + c0, L2E, ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b + c0));
+        if (hipEventRecord(P->ev_kv[l], ss) != hipSuccess) return fail(ERGM_EHIP, "model: event record");
+        ERGM_TRY(quant_block(l + 1));  // block l+1's weights before block l+1's K/V (its forward needs both)
+        return l == L - 1 ? side_tail() : ERGM_OK;
+    };
+    if (kvb) {
+        ERGM_TRY(kv_block(0));
+    } else {
+        {
             Probe pr(P, 4, ss);
             if (P->f8)
                 ERGM_TRY(gemm8(P, ss, T, L2E, E, P->qcap, P->scap, P->xcap, P->capkv8, P->capkv8_s, P->capkv8_x,
@@ -1245,19 +1259,17 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
                 ERGM_TRY(gemm(P, ss, T, L2E, E, P->cap, P->XE, ERGM_MK, p.capkv_w_b, L2E, ERGM_KN, P->kv_all, L2E,
                               ERGM_BF16, ERGM_EPI_BIAS, p.capkv_b));
         }
-        // the embedding backward's sort needs only the ids: done here, off the critical chain
-        if (train && !P->dry)
-            ERGM_TRY(embed_bwd_sort(P->ids, P->tt, P->cap_ids, T, d.vocab, P->keys, P->row_flag, d.vocab_pad, ss));
-        ERGM_TRY(side_mark(P, L));
-        if (!P->kv_per_block || P->dry)
-            for (int l = 1; l < L; ++l) ERGM_TRY(quant_block(l));
+        ERGM_TRY(side_tail());
+        for (int l = 1; l < L; ++l) ERGM_TRY(quant_block(l));
     }
     // Enqueue order: launch by launch, alternating chains.  The forward's kernels are short, so the host's enqueue
     // pace can set the GPU's: enqueued a block at a time, the chains ran one block after the other instead of side
     // by side (profiles/r01_overlap_experiments.txt).
     constexpr int NP = 11;  // fwd_block parts
-    for (int g = 0; g < L * NP; ++g)
+    for (int g = 0; g < L * NP; ++g) {
+        if (kvb && g % NP == 1 && g / NP + 1 < L) ERGM_TRY(kv_block(g / NP + 1));
         for (int c = 0; c < nchain; ++c) ERGM_TRY(fwd_block(P, g / NP, cs[c], bsplit[c], bsplit[c + 1] - bsplit[c], g % NP));
+    }
     for (int c = 1; c < nchain && !P->dry; ++c)
         if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
             return fail(ERGM_EHIP, "model: chain join");
