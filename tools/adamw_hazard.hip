@@ -1,5 +1,5 @@
 // AdamW hazard probe (gfx950): the production AdamW element pass (adamw.hip) against an exact host reference, alone and
-// beside MFMA waves on the same CUs.  tools/adamw_probe.py found replicas of the same update disagreeing in lanes 48-63
+// beside MFMA waves on the same CUs.  a replica probe (profiles/r06_adamw_replica_probe.txt) found replicas of the same update disagreeing in lanes 48-63
 // (float4 components 0 / 2, mostly exp_avg_sq) when AdamW overlapped GEMMs; this isolates the kernel: the same inputs
 // every iteration, outputs compared word for word with an IEEE float32 host computation (the kernel's arithmetic is all
 // correctly rounded: no FMA contraction, IEEE sqrt and division).

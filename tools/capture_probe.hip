@@ -1,5 +1,5 @@
 // Which part of the executor's three-stream fork/join pattern makes hipStreamEndCapture crash (round 6: a whole-step
-// capture of the training forward segfaults in EndCapture, profiles/r06_graph_capture.txt)?  Captures the forward's
+// capture of the training forward segfaults in EndCapture, profiles/r06_graph_capture_segv.txt)?  Captures the forward's
 // pattern — fork two streams off the capturing one with recorded events, one of them starting with a memset and
 // waiting for the other, join both back — with the events created under different flags, instantiates the graph and
 // replays it, checking the result.  Usage: capture_probe <variant>
