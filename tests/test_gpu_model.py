@@ -556,6 +556,32 @@ def test_grouped_weight_gradient_launches_are_bitwise_the_separate_ones(gpu, mon
     assert_bitwise(res[1][1], res[0][1], "grad", model.layout)
 
 
+@pytest.mark.parametrize("B,S,Lyr", [(16, 128, 3), (3, 32, 2), (1, 16, 1)])
+def test_step_scheduling_switches_are_bitwise_the_previous_schedule(gpu, monkeypatch, B, S, Lyr):
+    """Round 6's scheduling changes move work between streams, not arithmetic: the caption K/V projection as one
+    GEMM per block enqueued between the chains' launches (ERGM_KV_PER_BLOCK=1, default) against the single stacked
+    GEMM, and the LM-head weight gradient forked before the LM-head dX GEMM (ERGM_LMHEAD_DW_FIRST=1, default) against
+    after it — bitwise the loss, logits and every gradient, with dropout (B = 1: one forward chain, L = 1: the
+    projection's only block is also its last)."""
+    from ergm_amd.data import synthetic_batch
+    V, E = 512, 128
+    res = []
+    for kv, dwf in (("0", "0"), ("1", "1"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("ERGM_KV_PER_BLOCK", kv)
+        monkeypatch.setenv("ERGM_LMHEAD_DW_FIRST", dwf)
+        torch.manual_seed(13)
+        cfg = ERGMConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=2, n_positions=1024)
+        model = GPT2LMHeadModel(cfg, device=gpu)
+        model.load_state_dict(O.init_params(O.OracleConfig(vocab_size=V, n_embd=E, n_layer=Lyr, n_head=2,
+                                                           n_positions=1024), seed=71), strict=False)
+        batch = synthetic_batch(B, S, n_turns=3, feat_dim=E, seed=72, vocab_hi=V - 3, sp1=V - 2, sp2=V - 1, eos=V - 4)
+        out = _run(model, batch, gpu)
+        res.append((out.loss.detach().clone(), out.logits_bf16.clone(), model.flat.grad.clone()))
+    for r in res[1:]:
+        for n, x, y in zip(("loss", "logits", "grad"), r, res[0]):
+            assert_bitwise(x, y, n, model.layout)
+
+
 @pytest.mark.parametrize("B,S,E,drop", [(16, 128, 128, True), (3, 37, 128, True), (2, 64, 256, False), (1, 2, 128, True),
                                          (2, 100, 128, False)])
 def test_fused_attention_backward_is_bitwise_the_two_launches(gpu, monkeypatch, B, S, E, drop):
