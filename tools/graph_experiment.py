@@ -1,7 +1,7 @@
 """How much would HIP-graph capture of the whole training step save?  Times the C2 step eagerly and as a
 replayed graph of one captured step (LR frozen at capture time: a timing experiment, not a training
 mode).  Usage (GPU box): python tools/graph_experiment.py [step|fwdbwd|fwd]  (what is captured: the whole step,
-forward + backward without the optimizer, the training forward alone)"""
+forward + backward without the optimizer, the training forward alone) [batch] (default 16; 1 = one forward chain)"""
 import faulthandler
 import os
 import sys
@@ -24,7 +24,8 @@ def main():
     model.init_weights(seed=0)
     mode = sys.argv[1] if len(sys.argv) > 1 else "step"
     opt = FusedAdamW([model.flat], lr=2e-5, model=model, overlap=mode == "step")  # no updates inside fwdbwd
-    b = synthetic_batch(16, 128, n_turns=5, seed=1)
+    bsz = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    b = synthetic_batch(bsz, 128, n_turns=5, seed=1)
     kw = dict(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], labels=b["labels"],
               emotion_labels=b["emotion_labels"], caption_ids=b["caption_ids"], imgs=b["visual_feat"],
               auds=b["audio_feat"])
