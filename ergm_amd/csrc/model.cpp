@@ -771,6 +771,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     for (auto& e : P->ev_join) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     // two forward chains over the batch halves (one chain measured +3-5 %, three level, four +20 %: round 2)
     P->fwd_chains = 2;
+    if (const char* e = getenv("ERGM_FWD_CHAINS")) P->fwd_chains = std::max(1, std::min(2, atoi(e)));
     // two backward chains measured slower at C2 (6.27 vs 5.85 ms/step: the GPU is already throughput-
     // saturated and the host enqueue grows, profiles/r02_bwd_chains_ab.txt): ERGM_BWD_CHAINS=2 enables
     P->bwd_chains = 1;
@@ -1273,6 +1274,9 @@ int do_forward(ergm_model_plan* P, void* logits, float* emo_logits, float* out_l
     for (int c = 1; c < nchain && !P->dry; ++c)
         if (hipEventRecord(ev_done[c], cs[c]) != hipSuccess || hipStreamWaitEvent(s, ev_done[c], 0) != hipSuccess)
             return fail(ERGM_EHIP, "model: chain join");
+    // every stream's forward work joined into the caller's stream (the side stream's tail — the embedding backward's
+    // sort — long done by now; a captured forward must not leave it unjoined)
+    if (kvb) ERGM_TRY(join_side(P, s, L));
     if (!P->dry)
         ERGM_TRY(ergm_layernorm_fwd(P->resid[3 * L], p.ln_f_w, p.ln_f_b, P->lnf, P->mf, P->rf, T, E, d.eps, s));
     // tied LM head: logits = ln_f(h) · wteᵀ over the padded vocab (pad rows of wte are zero)
