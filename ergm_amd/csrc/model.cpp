@@ -804,6 +804,7 @@ extern "C" int ergm_model_create(const ergm_model_dims* dims, const ergm_model_p
     for (auto& e : P->ev_wq) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     P->kv_per_block = true;
     if (const char* e = getenv("ERGM_KV_PER_BLOCK")) P->kv_per_block = atoi(e) != 0;
+    if (const char* e = getenv("ERGM_OPT_LAG")) P->opt_lag = std::max(0, std::min(4, atoi(e)));  // A/B only
     P->ev_kv.assign(P->kv_per_block ? d.n_layer : 0, nullptr);
     for (auto& e : P->ev_kv) ok = ok && hipEventCreateWithFlags(&e, kSyncEv) == hipSuccess;
     if (!ok) {
