@@ -1740,7 +1740,11 @@ static GemmArgs make_args(const ergm_gemm_desc* d, const void* A, const void* B,
     // do not evict the operands of the kernels running beside the LM head (C2 step +0.5-1 %,
     // profiles/r01_overlap_experiments.txt #14) ... and so are the f32 weight gradients (A = activationsᵀ),
     // consumed later by the optimizer / the all-reduce (C5 +0.4-0.8 %, C2 neutral: #17)
-    a.nt_store = (d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
+    static const bool nt_wide = [] {  // ERGM_NT_WIDE=0: vocabulary-wide bf16 outputs (the logits) stored normally (A/B)
+        const char* e = getenv("ERGM_NT_WIDE");
+        return !e || atoi(e) != 0;
+    }();
+    a.nt_store = (nt_wide && d->c_dtype == ERGM_BF16 && d->N >= 32768) ||
                  (d->c_dtype == ERGM_F32 && d->a_layout == ERGM_KM && d->epilogue == ERGM_EPI_NONE);
     // the in-GEMM bias gradient runs in the pipelined (non-warp-specialised) kernels; others use a column-sum pass
     const bool cs_in = d->bias_grad && p.cfg >= 0 && kCfgs[p.cfg].np == 0 && kCfgs[p.cfg].ks == 1 && kCfgs[p.cfg].mf == 16;
